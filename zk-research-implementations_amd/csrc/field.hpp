@@ -1,0 +1,238 @@
+// Prime-field arithmetic shared by the host C++ and the gfx950 kernels.
+//
+// Element = 8 x 32-bit little-endian limbs in Montgomery form with R = 2^256,
+// i.e. the same 32-byte image as ark-ff 0.5.0's `Fp<MontBackend<_, 4>, 4>`
+// (4 x u64 LE limbs, Montgomery, R = 2^256), so a Rust caller's `Vec<F>`
+// memory is usable as-is (Cargo.lock:89-92 pins ark-ff 0.5.0; the field
+// operations it replaces are every `+ - *` in
+// multilinear_polynomial_evaluation.rs:52-110, composed_polynomial.rs:52-99,
+// sum_check_protocol.rs:25-166 and univariate_polynomial_dense.rs:20-74).
+//
+// Multiplication is word-serial Montgomery (CIOS) built on gfx950's
+// v_mad_u64_u32 (32x32+64 -> 64) and v_add_co/v_addc_co carry chains; every
+// operation returns a fully reduced value in [0, p), so canonical results
+// are bit-identical to ark-ff regardless of the internal schedule.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define ZK_HD __host__ __device__ __forceinline__
+#else
+#define ZK_HD static inline
+#endif
+
+namespace zk {
+
+enum FieldId : int { BN254_FR = 0, BN254_FQ = 1, BLS12_381_FR = 2 };
+
+// Public curve constants (ark-bn254 0.5.0 / ark-bls12-381 0.5.0, Cargo.lock:45-60).
+struct Bn254Fr {
+  static constexpr int id = BN254_FR;
+  static constexpr uint32_t P[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t PINV = 0xefffffffu;  // -p^-1 mod 2^32
+  static constexpr uint32_t R1[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                     0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+  static constexpr uint32_t INV2[8] = {0x1ffffffeu, 0x783c14d8u, 0x0c8d1eddu, 0xaf982f6fu,
+                                       0xfcfd4f45u, 0x8f5f7492u, 0x3d9cbfacu, 0x1f37631au};
+};
+struct Bn254Fq {
+  static constexpr int id = BN254_FQ;
+  static constexpr uint32_t P[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t PINV = 0xe4866389u;
+  static constexpr uint32_t R1[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                     0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+  static constexpr uint32_t INV2[8] = {0x4f060572u, 0x87bee7d2u, 0x2f1c6ae5u, 0xd0fd2addu,
+                                       0xfcfd4f44u, 0x8f5f7492u, 0x3d9cbfacu, 0x1f37631au};
+};
+struct Bls12_381Fr {
+  static constexpr int id = BLS12_381_FR;
+  static constexpr uint32_t P[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                    0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  static constexpr uint32_t PINV = 0xffffffffu;
+  static constexpr uint32_t R1[8] = {0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau,
+                                     0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u};
+  static constexpr uint32_t R2[8] = {0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu,
+                                     0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u};
+  static constexpr uint32_t INV2[8] = {0xffffffffu, 0x00000000u, 0x0001a401u, 0xac425bfdu,
+                                       0xf65e27fau, 0xccc627f7u, 0xd66282b7u, 0x0c1258acu};
+};
+
+struct Fe {
+  uint32_t v[8];
+};
+
+// ---- carry primitives ------------------------------------------------------
+ZK_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+#if defined(__clang__)
+  unsigned int c;
+  uint32_t r = __builtin_addc(a, b, cin, &c);
+  *cout = c;
+  return r;
+#else
+  uint64_t s = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+#endif
+}
+ZK_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+#if defined(__clang__)
+  unsigned int c;
+  uint32_t r = __builtin_subc(a, b, bin, &c);
+  *bout = c;
+  return r;
+#else
+  uint64_t d = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+#endif
+}
+// 32x32 + 32 -> 64 (maps to one v_mad_u64_u32 with a zero-extended addend)
+ZK_HD uint64_t mad64(uint32_t a, uint32_t b, uint32_t c) { return (uint64_t)a * b + c; }
+
+// ---- field operations ------------------------------------------------------
+template <class F>
+ZK_HD Fe fe_zero() {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = 0;
+  return r;
+}
+template <class F>
+ZK_HD Fe fe_one() {  // Montgomery image of 1 = R mod p
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = F::R1[i];
+  return r;
+}
+template <class F>
+ZK_HD Fe fe_inv2() {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = F::INV2[i];
+  return r;
+}
+
+// r = x - p if x >= p else x   (x < 2p, x < 2^256)
+template <class F>
+ZK_HD Fe fe_reduce_once(const Fe& x) {
+  Fe t;
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t.v[i] = subb32(x.v[i], F::P[i], b, &b);
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = b ? x.v[i] : t.v[i];
+  return r;
+}
+
+template <class F>
+ZK_HD Fe fe_add(const Fe& a, const Fe& b) {
+  // p < 2^255, so a + b < 2^256: no carry out of the top limb.
+  Fe s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.v[i] = addc32(a.v[i], b.v[i], c, &c);
+  return fe_reduce_once<F>(s);
+}
+
+template <class F>
+ZK_HD Fe fe_sub(const Fe& a, const Fe& b) {
+  Fe d;
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) d.v[i] = subb32(a.v[i], b.v[i], bw, &bw);
+  // if borrow: d += p (mask form keeps the wave uniform)
+  const uint32_t mask = 0u - bw;
+  uint32_t c = 0;
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = addc32(d.v[i], F::P[i] & mask, c, &c);
+  return r;
+}
+
+template <class F>
+ZK_HD Fe fe_dbl(const Fe& a) {
+  return fe_add<F>(a, a);
+}
+
+// Montgomery product a*b*R^-1 mod p, CIOS over 32-bit words.
+// Row A: u = t + a*b_i (8 mads on zero-extended t_j, then one carry chain
+// folding hi(P_{j-1}) into lo(P_j)). Row B: u += m*p, shift one word down.
+// Invariant t < 2p < 2^256 between rows (p < 2^255).
+template <class F>
+ZK_HD Fe fe_mul(const Fe& a, const Fe& b) {
+  uint32_t t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t bi = b.v[i];
+    uint64_t P[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) P[j] = mad64(a.v[j], bi, t[j]);
+    uint32_t u[9];
+    uint32_t c = 0;
+    u[0] = (uint32_t)P[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) u[j] = addc32((uint32_t)P[j], (uint32_t)(P[j - 1] >> 32), c, &c);
+    u[8] = (uint32_t)(P[7] >> 32) + c;
+    const uint32_t m = u[0] * F::PINV;
+    uint64_t Q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Q[j] = mad64(m, F::P[j], u[j]);
+    c = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) t[j - 1] = addc32((uint32_t)Q[j], (uint32_t)(Q[j - 1] >> 32), c, &c);
+    t[7] = u[8] + (uint32_t)(Q[7] >> 32) + c;
+  }
+  Fe r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.v[j] = t[j];
+  return fe_reduce_once<F>(r);
+}
+
+template <class F>
+ZK_HD Fe fe_to_mont(const Fe& canon) {  // canon < p
+  Fe r2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r2.v[i] = F::R2[i];
+  return fe_mul<F>(canon, r2);
+}
+template <class F>
+ZK_HD Fe fe_from_mont(const Fe& m) {
+  Fe one = fe_zero<F>();
+  one.v[0] = 1;
+  return fe_mul<F>(m, one);
+}
+
+template <class F>
+ZK_HD bool fe_is_zero(const Fe& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc |= a.v[i];
+  return acc == 0;
+}
+template <class F>
+ZK_HD bool fe_eq(const Fe& a, const Fe& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+// canonical < p ?
+template <class F>
+ZK_HD bool fe_is_canonical(const Fe& x) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) (void)subb32(x.v[i], F::P[i], b, &b);
+  return b != 0;
+}
+
+}  // namespace zk
