@@ -1,0 +1,251 @@
+"""Benchmark: GKR sum-check prover (BASELINE.json metric) on MI355X.
+
+One step = one full `gkr_prove` (sum_check_protocol.rs:86-115) over the
+composed polynomial A*S + M*P whose four tables are already resident in HBM
+(BASELINE config 3: 24 variables per GPU, BN254 Fr, synthetic uniform tables,
+seed 3). With --gpus N (torchrun, one process per GPU) the hypercube has
+24 + log2(N) variables, rank g holding the sub-cube whose low log2(N) index bits
+equal g; each round does one RCCL all-reduce of the partial sums (weak scaling:
+per-GPU table size fixed).
+
+value = canonical field ops / s of the whole job = 32 * (2^n - 1) * steps / time
+(SURVEY.md 8(d)); ms_per_step = prover milliseconds per proof.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zk-research-implementations_amd"))
+
+FIELDS = {"bn254_fr": 0, "bn254_fq": 1, "bls12_381_fr": 2}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nvars", type=int, default=24, help="variables per GPU")
+    ap.add_argument("--field", default="bn254_fr", choices=sorted(FIELDS))
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--cpu-sample-nvars", type=int, default=22)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fold", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(field: int, nvars: int) -> dict:
+    """Reference CPU path: the C restatement of the reference prover
+    (oracle/zk_oracle.c, same algorithm and allocation pattern as
+    sum_check_protocol.rs:86-166), single thread like the reference (no rayon),
+    timed on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle as co  # checker/baseline only
+
+    tabs = [co.synth(field, 3, t, 0, 1 << nvars) for t in range(4)]
+    t0 = time.perf_counter()
+    co.gkr_prove(field, tabs, co.Transcript())
+    dt = time.perf_counter() - t0
+    ops = 32.0 * ((1 << nvars) - 1)
+    return {
+        "value": ops / dt,
+        "unit": "field-ops/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"one gkr_prove over a {nvars}-var synthetic SumPoly (4 tables x 2^{nvars}), "
+        f"{dt:.2f} s single-thread, host '{cpu_model()}' ({os.cpu_count()} logical CPUs)",
+        "prover_ms_sample": dt * 1e3,
+    }
+
+
+def fold_bench(ctx, field: int, nvars: int = 20, reps: int = 10) -> dict:
+    """BASELINE config 2: one partial_evaluate(0, r) of a 20-var table. 10
+    distinct input/output buffer pairs (480 MiB > 256 MiB Infinity Cache) are
+    rotated so every launch streams from HBM."""
+    import ctypes as C
+
+    import numpy as np
+
+    from zk_amd._lib import check, lib
+    from zk_amd.elems import as_limbs, ptr
+
+    bufs = [(ctx.synth(field, 1 << nvars, seed=2, table=i), ctx.alloc(field, 1 << (nvars - 1))) for i in range(reps)]
+    r = ptr(as_limbs([12345678901234567890]))
+    for i, o in bufs[:2]:
+        check(lib().zk_dev_mle_partial_evaluate(ctx.h, field, i.ptr, nvars, 0, 0, r, o.ptr))
+    ctx.reset_stats()
+    ctx.set_timing(True)
+    for _ in range(3):
+        for i, o in bufs:
+            check(lib().zk_dev_mle_partial_evaluate(ctx.h, field, i.ptr, nvars, 0, 0, r, o.ptr))
+    ctx.set_timing(False)
+    k = ctx.stats()["kernels"]["fold"]
+    gbs = k["alg_bytes"] / (k["ms"] / 1e3) / 1e9
+    return {
+        "workload": f"partial_evaluate(0, r), {nvars}-var BN254 Fr, {reps} rotated buffers",
+        "launches": k["launches"],
+        "avg_launch_us": k["ms"] * 1e3 / k["launches"],
+        "bytes_per_launch": k["alg_bytes"] / k["launches"],
+        "achieved_GBs": gbs,
+        "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
+    }
+
+
+def main() -> None:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    field = FIELDS[args.field]
+
+    import ctypes as C
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+    from zk_amd.context import rccl_unique_id
+    from zk_amd.elems import as_limbs, ptr
+
+    torch.cuda.set_device(local)
+    ctx = zk_amd.Context(local)
+    lg = (world - 1).bit_length()
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        obj = [rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.attach_rccl(rank, world, obj[0])
+
+    nloc = args.nvars
+    n = nloc + lg
+    # this rank's shard: local m <-> global m*world + rank
+    tabs = [ctx.synth(field, 1 << nloc, seed=args.seed, table=t, index0=rank, stride=world) for t in range(4)]
+    arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
+    coeffs = np.zeros((n, 3, 4), np.uint64)
+    nco = np.zeros(n, np.uint8)
+    ch = np.zeros((n, 4), np.uint64)
+    zero = ptr(as_limbs([0]))
+
+    def step():
+        tr = zk_amd.Transcript(field)
+        check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, nloc, 0, zero, tr.h, ptr(coeffs), ptr(nco),
+                                                      ptr(ch)))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    first_challenges = ch.copy()
+    ctx.reset_stats()
+    ctx.set_timing(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    st = ctx.stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert np.array_equal(first_challenges, ch), "proof changed between steps"
+
+    ops = 32.0 * ((1 << n) - 1) * args.steps
+    value = ops / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+    k = st["kernels"]
+    rnd = k["gkr_round"]
+    achieved = rnd["alg_bytes"] / (rnd["ms"] / 1e3) / 1e9
+    kernel_ms = sum(v["ms"] for v in k.values()) / args.steps
+    muls = sum(v["field_muls"] for v in k.values()) / args.steps
+
+    if rank == 0:
+        out = {
+            "metric": "GKR sum-check field-ops/sec + prover ms, 24-var BN254, 1/2/4/8 GPU",
+            "value": value,
+            "unit": "field-ops/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u256 mod p (8x32-bit Montgomery limbs)",
+            "data": "synthetic (counter-based SplitMix64 tables mod p, device-generated; no dataset)",
+            "config": {
+                "workload": f"gkr_prove over SumPoly[A*S + M*P], {n} variables total "
+                f"({nloc} per GPU), {args.field}, seed {args.seed}, tables resident in HBM",
+                "field": args.field,
+                "nvars_total": n,
+                "nvars_per_gpu": nloc,
+                "parallelism": f"hypercube split over {world} GPU(s) by low index bits; "
+                "1 RCCL all-reduce (24 x u64) per round" if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_gkr_round (fused fold + round evaluation)",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "launches": rnd["launches"],
+                "avg_launch_us": rnd["ms"] * 1e3 / max(1, rnd["launches"]),
+                "alg_bytes_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]),
+            },
+            "breakdown_per_step": {
+                "wall_ms": ms_per_step,
+                "kernel_ms": kernel_ms,
+                "kernel_ms_by_kind": {kk: v["ms"] / args.steps for kk, v in k.items() if v["launches"]},
+                "host_syncs": st["host_syncs"] / args.steps,
+                "collectives": st["collectives"] / args.steps,
+                "field_muls": muls,
+                "modmul_rate_G_per_s_in_kernels": muls / (kernel_ms / 1e3) / 1e9 if kernel_ms else None,
+            },
+        }
+        if not args.no_fold:
+            out["fold_20var"] = fold_bench(ctx, field)
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(field, args.cpu_sample_nvars)
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu_baseline"] = value / cb["value"]
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+/*
+ * zk_sumcheck.h — C ABI of the MI355X-native sum-check / GKR sum-check prover.
+ *
+ * Drop-in boundary for the reference crates `sum_check`, `multilinear_polynomial`
+ * and `fiat_shamir` (obah/zk-research-implementations). Each entry point names
+ * the Rust item it replaces (paths relative to the reference root). The
+ * reference is generic over `F: PrimeField`; here the field is a runtime
+ * `zk_field` and elements are 32-byte little-endian 4 x u64 limbs, either
+ * canonical (what `fq_vec_to_bytes` serialises) or Montgomery (ark-ff 0.5.0's
+ * in-memory `Fp<MontBackend<_,4>,4>`, R = 2^256), selected per call by
+ * `zk_repr` so a Rust shim can pass `Vec<F>` memory directly.
+ *
+ * Conventions
+ *  - every function returns ZK_OK (0) or an error code; where the reference
+ *    would `panic!` (non-power-of-two tables, mismatched sizes, wrong number of
+ *    evaluation points) the call returns ZK_EINVAL and writes nothing else;
+ *  - verification failures are NOT errors: they return ZK_OK with
+ *    *out_verified = 0, exactly as the reference returns `false`;
+ *  - host buffers are caller-owned; `zk_dev_*` calls take HIP device pointers
+ *    holding Montgomery elements (32 B each, 16-B aligned);
+ *  - a zk_ctx is bound to one HIP device and is not thread-safe: one per
+ *    host thread. All calls are synchronous on return;
+ *  - compute runs on the GPU only. A ctx cannot be created without a usable
+ *    gfx950 device (ZK_EDEVICE); there is no CPU fallback.
+ */
+#ifndef ZK_SUMCHECK_H
+#define ZK_SUMCHECK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZK_ABI_VERSION 1u
+
+typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
+typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
+
+/* One field element: 4 x u64, little-endian limbs. */
+typedef struct {
+  uint64_t limb[4];
+} zk_fe;
+
+enum {
+  ZK_OK = 0,
+  ZK_EINVAL = 1,       /* reference would panic / bad argument */
+  ZK_EDEVICE = 2,      /* HIP error or no usable device */
+  ZK_ECOMM = 3,        /* collective failed */
+  ZK_ENOMEM = 4,       /* device or host allocation failed */
+  ZK_EUNSUPPORTED = 5  /* valid request outside what this build implements */
+};
+
+typedef struct zk_ctx zk_ctx;
+typedef struct zk_transcript zk_transcript;
+
+uint32_t zk_abi_version(void);
+/* Message describing the last failing call on this host thread ("" if none). */
+const char* zk_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Context: HIP device + stream + device workspace (+ optional communicator).
+ * ------------------------------------------------------------------------- */
+int zk_ctx_create(int device, zk_ctx** out);
+void zk_ctx_destroy(zk_ctx* ctx);
+
+/* Per-kernel-kind counters; timing (HIP events around every launch on the
+ * ctx stream) is collected only while enabled. */
+enum {
+  ZK_K_GKR_ROUND0 = 0, /* first GKR round: e0,e1,e2 over the input tables */
+  ZK_K_GKR_ROUND = 1,  /* fused fold-by-r + next-round e0,e2 over 4 tables */
+  ZK_K_SC_ROUND = 2,   /* plain sum-check: (fold) + half sums */
+  ZK_K_FOLD = 3,       /* MultilinearPoly::partial_evaluate */
+  ZK_K_REDUCE = 4,     /* block partials -> limb-split sums */
+  ZK_K_CONVERT = 5,    /* canonical <-> Montgomery */
+  ZK_K_SYNTH = 6,      /* synthetic table generator */
+  ZK_K_KINDS = 7
+};
+typedef struct {
+  uint64_t launches[ZK_K_KINDS];
+  double kernel_ms[ZK_K_KINDS];  /* sum of event-timed durations */
+  double alg_bytes[ZK_K_KINDS];  /* algorithmic HBM bytes */
+  double field_muls[ZK_K_KINDS]; /* Montgomery multiplications issued */
+  uint64_t host_syncs;           /* device->host round trips */
+  uint64_t collectives;          /* all-reduce / all-gather calls */
+} zk_stats;
+int zk_ctx_set_timing(zk_ctx* ctx, int enable);
+int zk_ctx_get_stats(const zk_ctx* ctx, zk_stats* out);
+int zk_ctx_reset_stats(zk_ctx* ctx);
+
+/* ---------------------------------------------------------------------------
+ * Fiat-Shamir transcript (host) — fiat_shamir/src/fiat_shamir_transcript.rs
+ * ------------------------------------------------------------------------- */
+zk_transcript* zk_transcript_new(void);                      /* Transcript::new        :12-17 */
+zk_transcript* zk_transcript_clone(const zk_transcript* t);  /* #[derive(Clone)]       :5     */
+void zk_transcript_free(zk_transcript* t);
+int zk_transcript_append(zk_transcript* t, const uint8_t* data, size_t len); /* append :19-21 */
+int zk_transcript_get_random_challenge(zk_transcript* t, zk_field field, zk_repr repr,
+                                       zk_fe* out);          /* get_random_challenge   :23-29 */
+/* fq_vec_to_bytes :32-37 — canonical LE, 32 bytes per element into out[32*n] */
+int zk_fe_vec_to_bytes(zk_field field, zk_repr repr, const zk_fe* v, size_t n, uint8_t* out);
+
+/* ---------------------------------------------------------------------------
+ * MultilinearPoly — multilinear_polynomial/src/multilinear_polynomial_evaluation.rs
+ * ------------------------------------------------------------------------- */
+/* partial_evaluate(bit, value) :52-63; out has 2^(nvars-1) elements */
+int zk_mle_partial_evaluate(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                            uint32_t bit, const zk_fe* value, zk_fe* out);
+/* evaluate(values) :79-91; npoint must equal nvars (else ZK_EINVAL, the panic at :80-82) */
+int zk_mle_evaluate(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                    const zk_fe* point, uint32_t npoint, zk_fe* out);
+
+/* ---------------------------------------------------------------------------
+ * Sum-check — sum_check/src/sum_check_protocol.rs
+ * ------------------------------------------------------------------------- */
+/* prove :25-52 -> Proof{proof_polynomials: nvars x [s0, s1], claimed_sum} */
+int zk_sumcheck_prove(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                      zk_fe* out_round_polys /* 2*nvars */, zk_fe* out_claimed_sum);
+/* verify :54-84; round_polys = nrounds polys of poly_len elements each */
+int zk_sumcheck_verify(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                       const zk_fe* round_polys, uint32_t nrounds, uint32_t poly_len, const zk_fe* claimed_sum,
+                       int* out_verified);
+/* gkr_prove :86-115 on SumPoly{[ProductPoly[t0,t1], ProductPoly[t2,t3]]}
+ * (composed_polynomial.rs:88-103 — reduce uses exactly these four tables).
+ * Mutates `transcript`; out_coeffs[3*k .. 3*k+ncoeffs[k]) are round k's trimmed
+ * UnivariatePoly coefficients; claimed_sum is passed through (:110-114). */
+int zk_gkr_sumcheck_prove(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* const tables[4], uint32_t nvars,
+                          const zk_fe* claimed_sum, zk_transcript* transcript, zk_fe* out_coeffs /* 3*nvars */,
+                          uint8_t* out_ncoeffs /* nvars */, zk_fe* out_challenges /* nvars */,
+                          zk_fe* out_claimed_sum);
+/* gkr_verify :117-150 (host-only, O(nrounds)). On failure *out_verified=0,
+ * final claim 0 and a single zero challenge (:128-134). out_challenges needs
+ * max(nrounds,1) slots. */
+int zk_gkr_sumcheck_verify(zk_field field, zk_repr repr, const zk_fe* coeffs /* 3*nrounds */,
+                           const uint8_t* ncoeffs, uint32_t nrounds, const zk_fe* claimed_sum,
+                           zk_transcript* transcript, int* out_verified, zk_fe* out_final_claimed_sum,
+                           zk_fe* out_challenges);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident API (tables already in HBM, Montgomery form)
+ * ------------------------------------------------------------------------- */
+int zk_dev_alloc(zk_ctx* ctx, size_t bytes, void** out);
+int zk_dev_free(zk_ctx* ctx, void* p);
+/* host (repr) -> device Montgomery, and back */
+int zk_dev_upload(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* host, size_t n, void* dev);
+int zk_dev_download(zk_ctx* ctx, zk_field field, zk_repr repr, const void* dev, size_t n, zk_fe* host);
+/* synthetic table: dev[m] = synth(seed, table, index0 + m*stride) in Montgomery form */
+int zk_dev_synth_fill(zk_ctx* ctx, zk_field field, void* dev, uint64_t count, uint64_t seed, uint32_t table,
+                      uint64_t index0, uint64_t stride);
+/* partial_evaluate on device buffers: d_out has 2^(nvars-1) elements (may not alias d_in) */
+int zk_dev_mle_partial_evaluate(zk_ctx* ctx, zk_field field, const void* d_in, uint32_t nvars, uint32_t bit,
+                                zk_repr repr, const zk_fe* value, void* d_out);
+/* gkr_prove over device tables (read-only; the ctx workspace holds the folds) */
+int zk_dev_gkr_sumcheck_prove(zk_ctx* ctx, zk_field field, const void* const d_tables[4], uint32_t nvars,
+                              zk_repr repr, const zk_fe* claimed_sum, zk_transcript* transcript,
+                              zk_fe* out_coeffs, uint8_t* out_ncoeffs, zk_fe* out_challenges);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU: the hypercube is split over `world` ranks (one process or thread
+ * per GPU, world a power of two). Rank g holds the sub-cube whose LOW
+ * log2(world) index bits equal g: local m <-> global m*world + g. The first
+ * nvars_local rounds fold purely locally; each round's partial sums are
+ * combined with ONE all-reduce of 24 u64 (three elements split into 32-bit
+ * limbs, exact); one all-gather of 4 elements per rank then lets every rank
+ * finish the last log2(world) rounds identically. No broadcast is needed:
+ * every rank derives the same challenges from the same transcript.
+ * ------------------------------------------------------------------------- */
+/* host-memory collectives supplied by the caller (e.g. torch.distributed/gloo) */
+typedef int (*zk_allreduce_u64_fn)(void* user, uint64_t* data, size_t count);          /* in-place SUM */
+typedef int (*zk_allgather_fn)(void* user, const void* send, void* recv, size_t bytes); /* rank-ordered */
+int zk_ctx_attach_host_comm(zk_ctx* ctx, int rank, int world, zk_allreduce_u64_fn allreduce,
+                            zk_allgather_fn allgather, void* user);
+/* RCCL over xGMI: rank 0 creates the id, every rank passes the same 128 bytes */
+int zk_comm_get_unique_id(uint8_t out[128]);
+int zk_ctx_attach_rccl(zk_ctx* ctx, int rank, int world, const uint8_t unique_id[128]);
+int zk_ctx_detach_comm(zk_ctx* ctx);
+/* gkr_prove over the global (nvars_local + log2(world))-variable SumPoly whose
+ * local shard this rank holds; outputs are the global proof (identical on all
+ * ranks). out arrays sized for nvars_local + log2(world) rounds. */
+int zk_dev_gkr_sumcheck_prove_sharded(zk_ctx* ctx, zk_field field, const void* const d_local_tables[4],
+                                      uint32_t nvars_local, zk_repr repr, const zk_fe* claimed_sum,
+                                      zk_transcript* transcript, zk_fe* out_coeffs, uint8_t* out_ncoeffs,
+                                      zk_fe* out_challenges);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZK_SUMCHECK_H */

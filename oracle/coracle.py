@@ -46,6 +46,9 @@ def lib():
         L.or_gkr_verify.argtypes = [i32, P, P, u32, P, P, P, P]
         L.or_synth_fill.argtypes = [i32, u64, u32, u64, u64, P]
         L.or_fe_from_le_bytes_mod_order.argtypes = [i32, P, C.c_size_t, P]
+        L.or_fe_to_mont.argtypes = [i32, P, P]
+        L.or_fe_add.argtypes = [i32, P, P, P]
+        L.or_fe_mul.argtypes = [i32, P, P, P]
         _lib = L
     return _lib
 

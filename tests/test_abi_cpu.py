@@ -1,0 +1,147 @@
+"""CPU checks of the product library: it loads, exports every symbol that
+include/zk_sumcheck.h declares, refuses to run compute without a GPU, and
+its host-side logic (transcript, serialisation, gkr_verify) matches the oracle."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import coracle as co
+import pyoracle as po
+from conftest import ROOT
+
+import zk_amd
+from zk_amd import _lib
+from zk_amd.elems import as_limbs, ptr, to_ints
+
+HEADER = os.path.join(ROOT, "include", "zk_sumcheck.h")
+
+
+def declared_functions() -> list[str]:
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    names = re.findall(r"\b(zk_[a-z0-9_]+)\s*\(", src)
+    return sorted(set(n for n in names if not n.endswith("_fn")))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 25
+    for n in names:
+        assert hasattr(lib, n), f"missing export {n}"
+    assert set(names) == set(_lib.SIGNATURES), "binding table out of sync with the header"
+
+
+def test_abi_version():
+    assert _lib.lib().zk_abi_version() == 1
+
+
+def test_nm_exports_match_header():
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (zk_[a-z0-9_]+)$", out, flags=re.M))
+    assert set(declared_functions()) <= exported
+
+
+def _gpu_present() -> bool:
+    return os.path.exists("/dev/kfd") and bool([d for d in os.listdir("/dev/dri")] if os.path.exists("/dev/dri") else [])
+
+
+@pytest.mark.skipif(_gpu_present(), reason="this host has a GPU")
+def test_no_gpu_means_loud_failure():
+    h = C.c_void_p()
+    rc = _lib.lib().zk_ctx_create(0, C.byref(h))
+    assert rc == _lib.ZK_EDEVICE
+    assert b"no CPU fallback" in _lib.lib().zk_last_error() or b"device" in _lib.lib().zk_last_error()
+    with pytest.raises(zk_amd.ZkError):
+        zk_amd.Context(0)
+
+
+# --- host logic vs oracle ------------------------------------------------------
+@pytest.mark.parametrize("field", [0, 1, 2])
+def test_transcript_matches_oracle(field):
+    t = zk_amd.Transcript(field)
+    o = po.Transcript(field)
+    for chunk in [b"zero knowledge", b"", bytes(range(200)), b"\x01" * 136, b"x" * 500]:
+        t.append(chunk)
+        o.append(chunk)
+        assert t.get_random_challenge() == o.get_random_challenge()
+    t2 = t.clone()
+    assert t2.get_random_challenge() == t.get_random_challenge()
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+def test_fq_vec_to_bytes_matches_oracle(field):
+    vals = po.synth(field, 5, 0, 0, 9) + [0, 1, po.MODULI[field] - 1]
+    assert zk_amd.fq_vec_to_bytes(vals, field) == po.fq_vec_to_bytes(vals)
+    with pytest.raises(ValueError):
+        zk_amd.fq_vec_to_bytes([po.MODULI[field]], field)  # >= p is not a field element
+
+
+def test_montgomery_repr_roundtrip_through_transcript():
+    # challenge in Montgomery repr == to_mont(canonical challenge)
+    L = _lib.lib()
+    for f in range(3):
+        ta, tb = L.zk_transcript_new(), L.zk_transcript_new()
+        a, b = np.zeros((1, 4), np.uint64), np.zeros((1, 4), np.uint64)
+        L.zk_transcript_get_random_challenge(ta, f, 0, ptr(a))
+        L.zk_transcript_get_random_challenge(tb, f, 1, ptr(b))
+        m = np.zeros((1, 4), np.uint64)
+        co.lib().or_fe_to_mont(f, a.ctypes.data, m.ctypes.data)
+        assert np.array_equal(m, b)
+        L.zk_transcript_free(ta)
+        L.zk_transcript_free(tb)
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+def test_gkr_verify_matches_oracle(field, golden):
+    g = golden["gkr_prove_10"][field]
+    polys = [[int(c, 16) for c in p] for p in g["round_polys"]]
+    claim = int(g["claimed_sum"], 16)
+    res = zk_amd.gkr_verify([zk_amd.UnivariatePoly(p, field) for p in polys], claim, zk_amd.Transcript(field))
+    assert res.verified and res.final_claimed_sum == int(g["final_claim"], 16)
+    assert res.random_challenges == [int(c, 16) for c in g["challenges"]]
+    bad = zk_amd.gkr_verify([zk_amd.UnivariatePoly(p, field) for p in polys], claim + 1, zk_amd.Transcript(field))
+    assert not bad.verified and bad.final_claimed_sum == 0 and bad.random_challenges == [0]
+
+
+def test_gkr_verify_reference_kat():  # sum_check_protocol.rs:247-269 via golden
+    tabs = [[0, 0, 0, 2], [0, 0, 0, 3], [0, 0, 0, 2], [0, 0, 0, 3]]
+    polys, cs, chal = po.gkr_prove(1, 12, tabs, po.Transcript(1))
+    v = zk_amd.gkr_verify([zk_amd.UnivariatePoly(p, 1) for p in polys], cs, zk_amd.Transcript(1))
+    assert v.verified and v.random_challenges == chal
+
+
+def test_gkr_verify_empty_and_trimmed_polys():
+    # zero round polynomial (all coefficients trimmed) is valid for claim 0
+    v = zk_amd.gkr_verify([zk_amd.UnivariatePoly([], 0)], 0, zk_amd.Transcript(0))
+    ok, fin, ch = po.gkr_verify(0, [[]], 0, po.Transcript(0))
+    assert v.verified == ok and v.final_claimed_sum == fin and v.random_challenges == ch
+    v0 = zk_amd.gkr_verify([], 5, zk_amd.Transcript(0))
+    assert v0.verified and v0.final_claimed_sum == 5 and v0.random_challenges == []
+
+
+def test_reference_shaped_constructors_panic_like_reference():
+    with pytest.raises(ValueError):
+        zk_amd.MultilinearPoly([1, 2, 3])
+    with pytest.raises(ValueError):
+        zk_amd.MultilinearPoly([])
+    with pytest.raises(ValueError):  # composed_polynomial.rs:357-374
+        zk_amd.ProductPoly([[0, 0, 0, 3], [0, 0, 0, 4, 0, 0, 0, 4]])
+    pp = zk_amd.ProductPoly([[0, 0, 0, 3]])
+    with pytest.raises(ValueError):
+        zk_amd.SumPoly([pp, zk_amd.ProductPoly([[1, 2], [3, 4]])])
+    with pytest.raises(ValueError):  # reduce() indexes polys[1]
+        zk_amd.SumPoly([zk_amd.ProductPoly([[1, 2], [3, 4]])]).gkr_tables()
+
+
+def test_limbs_roundtrip():
+    vals = [0, 1, (1 << 254) + 12345, (1 << 64) - 1]
+    assert to_ints(as_limbs(vals)) == vals

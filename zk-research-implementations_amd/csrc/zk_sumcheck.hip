@@ -1,0 +1,1057 @@
+// MI355X-native sum-check / GKR sum-check prover: host orchestration of the
+// gfx950 kernels in kernels.hpp behind the C ABI of include/zk_sumcheck.h.
+//
+// Round structure:
+//   GKR  (sum_check_protocol.rs:86-115): round 0 = k_gkr_round0 (e0,e1,e2);
+//        round k>=1 = k_gkr_round (fold by r_{k-1} + e0,e2) -> k_reduce_partials
+//        -> 96 B D2H -> host: e1 = s_{k-1}(r_{k-1}) - e0, closed-form
+//        interpolation + trim, Keccak absorb, challenge r_k.
+//   plain (sum_check_protocol.rs:25-52): k_sc_round (fold + half sums).
+// The host side holds only O(1)-per-round scalar work and the transcript;
+// every table-sized operation runs on the GPU.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/zk_sumcheck.h"
+#include "field.hpp"
+#include "keccak.hpp"
+#include "kernels.hpp"
+
+using zk::Fe;
+
+// ===========================================================================
+// errors
+// ===========================================================================
+namespace {
+thread_local std::string g_last_error;
+
+struct ZkError {
+  int code;
+  std::string msg;
+};
+[[noreturn]] void fail(int code, const std::string& msg) { throw ZkError{code, msg}; }
+
+#define HIPCK(x)                                                                        \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) fail(ZK_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define NCCLCK(x)                                                                            \
+  do {                                                                                       \
+    ncclResult_t r_ = (x);                                                                   \
+    if (r_ != ncclSuccess) fail(ZK_ECOMM, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+template <class Fn>
+int guarded(Fn&& fn) {
+  try {
+    fn();
+    g_last_error.clear();
+    return ZK_OK;
+  } catch (const ZkError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return ZK_ENOMEM;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return ZK_EDEVICE;
+  }
+}
+
+void require(bool cond, const char* msg) {
+  if (!cond) fail(ZK_EINVAL, msg);
+}
+
+// runtime field -> compile-time parameter set
+template <class Fn>
+void dispatch(zk_field field, Fn&& fn) {
+  switch (field) {
+    case ZK_BN254_FR: fn(zk::Bn254Fr{}); break;
+    case ZK_BN254_FQ: fn(zk::Bn254Fq{}); break;
+    case ZK_BLS12_381_FR: fn(zk::Bls12_381Fr{}); break;
+    default: fail(ZK_EINVAL, "unknown field");
+  }
+}
+
+// zk_fe (4 x u64 LE) <-> Fe (8 x u32 LE): same bytes on a little-endian host
+inline Fe from_zk(const zk_fe& a) {
+  Fe r;
+  memcpy(r.v, a.limb, 32);
+  return r;
+}
+inline zk_fe to_zk(const Fe& a) {
+  zk_fe r;
+  memcpy(r.limb, a.v, 32);
+  return r;
+}
+
+template <class F>
+Fe in_mont(zk_repr repr, const zk_fe& a) {  // host scalar in -> Montgomery
+  Fe x = from_zk(a);
+  require(zk::fe_is_canonical<F>(x), "field element >= modulus");
+  return repr == ZK_REPR_MONTGOMERY ? x : zk::fe_to_mont<F>(x);
+}
+template <class F>
+zk_fe out_repr(zk_repr repr, const Fe& m) {  // Montgomery -> host scalar out
+  return to_zk(repr == ZK_REPR_MONTGOMERY ? m : zk::fe_from_mont<F>(m));
+}
+template <class F>
+void canon_bytes(const Fe& m, uint8_t out[32]) {  // into_bigint().to_bytes_le()
+  const Fe c = zk::fe_from_mont<F>(m);
+  memcpy(out, c.v, 32);
+}
+
+}  // namespace
+
+// ===========================================================================
+// transcript (fiat_shamir_transcript.rs:5-37)
+// ===========================================================================
+struct zk_transcript {
+  zk::Keccak256 h;
+};
+
+namespace {
+// get_random_challenge: d = finalize_reset(); append(d); from_le_bytes_mod_order(d)
+template <class F>
+Fe challenge(zk_transcript* t) {
+  uint8_t d[32];
+  t->h.finalize_reset(d);
+  t->h.update(d, 32);
+  Fe x;
+  memcpy(x.v, d, 32);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) x = zk::fe_reduce_once<F>(x);  // 2^256 < 6p
+  return zk::fe_to_mont<F>(x);
+}
+template <class F>
+void absorb(zk_transcript* t, const Fe* m, size_t n) {  // append(fq_vec_to_bytes(v))
+  uint8_t b[32];
+  for (size_t i = 0; i < n; ++i) {
+    canon_bytes<F>(m[i], b);
+    t->h.update(b, 32);
+  }
+}
+}  // namespace
+
+// ===========================================================================
+// context
+// ===========================================================================
+namespace {
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) HIPCK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, b) != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      fail(ZK_ENOMEM, "hipMalloc of " + std::to_string(b) + " bytes failed");
+    }
+    bytes = b;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  Fe* fe(size_t off_elems = 0) const { return reinterpret_cast<Fe*>(p) + off_elems; }
+};
+
+enum CommKind { COMM_NONE = 0, COMM_HOST = 1, COMM_RCCL = 2 };
+}  // namespace
+
+struct zk_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  DevBuf work[2];  // ping-pong fold workspaces: 4 tables each
+  DevBuf input;    // host-API staging (4 tables)
+  DevBuf partials;
+  DevBuf small;    // reduce output (u64[32]) + flag + gather buffers
+  uint64_t* h_red = nullptr;  // pinned readback
+  bool timing = false;
+  zk_stats stats{};
+  struct Pending {
+    int kind;
+    hipEvent_t a, b;
+  };
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free;
+  std::vector<Pending> pending;
+  // communicator
+  int rank = 0, world = 1;
+  CommKind comm = COMM_NONE;
+  zk_allreduce_u64_fn ar = nullptr;
+  zk_allgather_fn ag = nullptr;
+  void* user = nullptr;
+  ncclComm_t nccl = nullptr;
+};
+
+namespace {
+constexpr size_t kSmallBytes = 64 * 1024;
+uint64_t* d_red(zk_ctx* c) { return reinterpret_cast<uint64_t*>(c->small.p); }
+uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 512); }
+char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 1024; }
+
+void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
+
+uint32_t grid_for(zk_ctx* c, uint64_t work) {
+  const uint64_t cap = (uint64_t)c->num_cus * 8;
+  uint64_t g = (work + zk::kBlock - 1) / zk::kBlock;
+  if (g < 1) g = 1;
+  return (uint32_t)std::min<uint64_t>(g, cap);
+}
+
+// Launch wrapper: counts algorithmic bytes / multiplications per kernel kind
+// and, when timing is on, brackets the launch with HIP events on c->stream.
+template <class L>
+void launch(zk_ctx* c, int kind, double bytes, double muls, L&& body) {
+  zk_ctx::Pending p{kind, nullptr, nullptr};
+  if (c->timing) {
+    if (c->ev_free.empty()) {
+      hipEvent_t a, b;
+      HIPCK(hipEventCreate(&a));
+      HIPCK(hipEventCreate(&b));
+      c->ev_free.push_back({a, b});
+    }
+    p.a = c->ev_free.back().first;
+    p.b = c->ev_free.back().second;
+    c->ev_free.pop_back();
+    HIPCK(hipEventRecord(p.a, c->stream));
+  }
+  body();
+  HIPCK(hipGetLastError());
+  if (c->timing) {
+    HIPCK(hipEventRecord(p.b, c->stream));
+    c->pending.push_back(p);
+  }
+  c->stats.launches[kind] += 1;
+  c->stats.alg_bytes[kind] += bytes;
+  c->stats.field_muls[kind] += muls;
+}
+// after a stream sync: fold event timings into the stats
+void flush_timing(zk_ctx* c) {
+  for (auto& p : c->pending) {
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
+    c->stats.kernel_ms[p.kind] += ms;
+    c->ev_free.push_back({p.a, p.b});
+  }
+  c->pending.clear();
+}
+void sync(zk_ctx* c) {
+  HIPCK(hipStreamSynchronize(c->stream));
+  c->stats.host_syncs += 1;
+  flush_timing(c);
+}
+
+// limb-split sum (8 x u64 holding 32-bit limbs, possibly summed over ranks)
+// -> field element: lo256 mod p + hi * 2^256 mod p.
+template <class F>
+Fe from_limb_sums(const uint64_t* w) {
+  uint32_t v[9];
+  uint64_t carry = 0;
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t s = w[i] + carry;
+    v[i] = (uint32_t)s;
+    carry = s >> 32;
+  }
+  v[8] = (uint32_t)carry;
+  Fe lo;
+  memcpy(lo.v, v, 32);
+  for (int i = 0; i < 5; ++i) lo = zk::fe_reduce_once<F>(lo);
+  if (v[8] == 0) return lo;
+  Fe hi = zk::fe_zero<F>();
+  hi.v[0] = v[8];
+  Fe r2;
+  for (int i = 0; i < 8; ++i) r2.v[i] = F::R2[i];
+  return zk::fe_add<F>(lo, zk::fe_mul<F>(hi, r2));  // hi * R mod p
+}
+
+// ---------------------------------------------------------------------------
+// partial sums: block partials (already written by the round kernel) ->
+// K limb-split sums -> [all-reduce over ranks] -> host field elements
+// ---------------------------------------------------------------------------
+template <class F, int K>
+void read_sums(zk_ctx* c, uint32_t nblk, bool across_ranks, Fe (&out)[K]) {
+  launch(c, ZK_K_REDUCE, (double)nblk * K * 32, 0,
+         [&] { zk::k_reduce_partials<F, K><<<1, zk::kBlock, 0, c->stream>>>(c->partials.fe(), nblk, d_red(c)); });
+  const bool multi = across_ranks && c->world > 1;
+  if (multi && c->comm == COMM_RCCL) {
+    NCCLCK(ncclAllReduce(d_red(c), d_red(c), K * 8, ncclUint64, ncclSum, c->nccl, c->stream));
+    c->stats.collectives += 1;
+  }
+  HIPCK(hipMemcpyAsync(c->h_red, d_red(c), K * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  if (multi && c->comm == COMM_HOST) {
+    if (c->ar(c->user, c->h_red, K * 8) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+    c->stats.collectives += 1;
+  }
+  for (int k = 0; k < K; ++k) out[k] = from_limb_sums<F>(c->h_red + 8 * k);
+}
+
+void ensure_partials(zk_ctx* c) { c->partials.ensure((size_t)c->num_cus * 8 * 3 * 32); }
+
+// ---------------------------------------------------------------------------
+// GKR sum-check rounds
+// ---------------------------------------------------------------------------
+struct GkrOut {
+  std::vector<Fe> coeffs;     // 3 per round (Montgomery), trimmed count in ncoeffs
+  std::vector<uint8_t> ncoeffs;
+  std::vector<Fe> challenges;
+};
+
+// Round polynomial through (0,e0),(1,e1),(2,e2) — the unique degree<=2
+// polynomial UnivariatePoly::interpolate returns (univariate_polynomial_dense.rs:48-74),
+// trailing zero coefficients trimmed (:14-18). Absorbs it, draws r_k and
+// returns s_k(r_k).
+template <class F>
+Fe finish_round(zk_transcript* tr, const Fe& e0, const Fe& e1, const Fe& e2, uint32_t k, GkrOut& out, Fe& r) {
+  using namespace zk;
+  Fe c[3];
+  c[0] = e0;
+  c[2] = fe_mul<F>(fe_add<F>(fe_sub<F>(e0, fe_dbl<F>(e1)), e2), fe_inv2<F>());
+  c[1] = fe_sub<F>(fe_sub<F>(e1, e0), c[2]);
+  int m = 3;
+  while (m > 0 && fe_is_zero<F>(c[m - 1])) --m;
+  absorb<F>(tr, c, (size_t)m);
+  out.ncoeffs[k] = (uint8_t)m;
+  for (int i = 0; i < 3; ++i) out.coeffs[3 * k + i] = i < m ? c[i] : fe_zero<F>();
+  r = challenge<F>(tr);
+  out.challenges[k] = r;
+  // UnivariatePoly::evaluate(r) (:20-26) via Horner — same field value
+  return fe_add<F>(c[0], fe_mul<F>(r, fe_add<F>(c[1], fe_mul<F>(r, c[2]))));
+}
+
+// Run `nv` rounds over 4 device tables of 2^nv elements starting at global
+// round k0. The first round of a phase computes e0,e1,e2 directly; later
+// rounds fold by the previous challenge in the same kernel. On return `cur`
+// points at the (unfolded) size-2 tables of the last round.
+template <class F>
+void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
+               GkrOut& out, Fe& claim, Fe& r) {
+  const uint64_t L = (uint64_t)1 << nv;
+  for (uint32_t i = 0; i < nv; ++i) {
+    const uint32_t k = k0 + i;
+    const uint64_t size = L >> i;  // table length in this round
+    const uint64_t h = size / 2;   // pairs
+    const uint32_t grid = grid_for(c, h);
+    Fe e0, e1, e2;
+    if (i == 0) {
+      launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, [&] {
+        zk::k_gkr_round0<F><<<grid, zk::kBlock, 0, c->stream>>>(cur[0], cur[1], cur[2], cur[3], h, c->partials.fe());
+      });
+      Fe s[3];
+      read_sums<F, 3>(c, grid, across_ranks, s);
+      e0 = s[0];
+      e1 = s[1];
+      e2 = s[2];
+    } else {
+      // fold previous (size 2*size) -> work[(i+1)&1] (size `size`) and evaluate;
+      // work[0] holds the size-L/2 level, work[1] the size-L/4 level, ...
+      Fe* w = c->work[(i + 1) & 1].fe();
+      Fe* nx[4] = {w, w + size, w + 2 * size, w + 3 * size};
+      const Fe rr = r;
+      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, [&] {
+        zk::k_gkr_round<F><<<grid, zk::kBlock, 0, c->stream>>>(cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2],
+                                                               nx[3], h, rr, c->partials.fe());
+      });
+      for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+      Fe s[2];
+      read_sums<F, 2>(c, grid, across_ranks, s);
+      e0 = s[0];
+      e2 = s[1];
+      // s_{k-1}(X) = sum_j f(X, j) is exact (degree 2 in X), so
+      // e0 + e1 = s_{k-1}(r_{k-1}) on the folded tables.
+      e1 = zk::fe_sub<F>(claim, e0);
+    }
+    claim = finish_round<F>(tr, e0, e1, e2, k, out, r);
+  }
+}
+
+template <class F>
+void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool sharded, zk_transcript* tr, GkrOut& out) {
+  const int G = sharded ? c->world : 1;
+  uint32_t lg = 0;
+  while ((1 << lg) < G) ++lg;
+  const uint32_t n = nloc + lg;
+  out.coeffs.assign(3 * (size_t)n, zk::fe_zero<F>());
+  out.ncoeffs.assign(n, 0);
+  out.challenges.assign(n, zk::fe_zero<F>());
+  if (n == 0) return;
+  ensure_partials(c);
+  const uint64_t Lloc = (uint64_t)1 << nloc;
+  const uint64_t wmax = std::max<uint64_t>(Lloc / 2, (uint64_t)G);
+  c->work[0].ensure(4 * wmax * 32);
+  c->work[1].ensure(4 * std::max<uint64_t>(wmax / 2, 1) * 32);
+  const Fe* cur[4] = {dT[0], dT[1], dT[2], dT[3]};
+  Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
+  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r);
+  if (lg == 0) return;
+
+  // ---- multi-GPU tail: every rank now holds 1 (folded) element per table ----
+  Fe* send = reinterpret_cast<Fe*>(d_gather(c));  // 4 elements
+  if (nloc > 0) {
+    Fe* s4[4] = {send, send + 1, send + 2, send + 3};
+    const Fe rr = r;
+    launch(c, ZK_K_FOLD, 4 * 96.0, 4.0, [&] {
+      zk::k_fold4<F><<<1, zk::kBlock, 0, c->stream>>>(cur[0], cur[1], cur[2], cur[3], s4[0], s4[1], s4[2], s4[3],
+                                                      1, rr);
+    });
+  } else {
+    for (int t = 0; t < 4; ++t)
+      HIPCK(hipMemcpyAsync(send + t, cur[t], 32, hipMemcpyDeviceToDevice, c->stream));
+  }
+  std::vector<Fe> gathered((size_t)G * 4);
+  if (c->comm == COMM_RCCL) {
+    Fe* recv = send + 4;
+    NCCLCK(ncclAllGather(send, recv, 4 * 32, ncclUint8, c->nccl, c->stream));
+    c->stats.collectives += 1;
+    HIPCK(hipMemcpyAsync(gathered.data(), recv, (size_t)G * 128, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+  } else {
+    Fe mine[4];
+    HIPCK(hipMemcpyAsync(mine, send, 128, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    if (c->comm != COMM_HOST || c->ag(c->user, mine, gathered.data(), 128) != 0)
+      fail(ZK_ECOMM, "all-gather failed");
+    c->stats.collectives += 1;
+  }
+  // global table t, index g = rank g's element (local index 0 <-> global g)
+  std::vector<Fe> tabs((size_t)4 * G);
+  for (int g = 0; g < G; ++g)
+    for (int t = 0; t < 4; ++t) tabs[(size_t)t * G + g] = gathered[(size_t)g * 4 + t];
+  Fe* stage = send + 4 + 4 * G;  // after the send/recv records in the gather area
+  HIPCK(hipMemcpyAsync(stage, tabs.data(), tabs.size() * 32, hipMemcpyHostToDevice, c->stream));
+  const Fe* tcur[4] = {stage, stage + G, stage + 2 * G, stage + 3 * G};
+  gkr_phase<F>(c, tcur, lg, nloc, false, tr, out, claim, r);
+}
+
+// ---------------------------------------------------------------------------
+// plain sum-check
+// ---------------------------------------------------------------------------
+template <class F>
+void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, const uint8_t* table_bytes,
+                     size_t nbytes, Fe* rp, Fe& claimed) {
+  // The transcript absorbs the whole table first (sum_check_protocol.rs:27):
+  // a serial host Keccak. Round 0's half sums are launched before it so the
+  // GPU works underneath the hash.
+  ensure_partials(c);
+  const uint64_t N = (uint64_t)1 << n;
+  if (n == 0) {
+    tr->h.update(table_bytes, nbytes);
+    HIPCK(hipMemcpyAsync(&claimed, dX, 32, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    absorb<F>(tr, &claimed, 1);
+    return;
+  }
+  c->work[0].ensure(std::max<uint64_t>(N / 2, 1) * 32);
+  c->work[1].ensure(std::max<uint64_t>(N / 4, 1) * 32);
+  uint64_t h = N / 2;
+  uint32_t grid = grid_for(c, h);
+  launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, [&] {
+    zk::k_sc_round<F, true><<<grid, zk::kBlock, 0, c->stream>>>(dX, nullptr, h, zk::fe_zero<F>(), c->partials.fe());
+  });
+  tr->h.update(table_bytes, nbytes);
+  Fe s[2];
+  read_sums<F, 2>(c, grid, false, s);
+  claimed = zk::fe_add<F>(s[0], s[1]);  // = sum of the table (:29)
+  absorb<F>(tr, &claimed, 1);
+  const Fe* cur = dX;
+  Fe r = zk::fe_zero<F>();
+  for (uint32_t k = 0; k < n; ++k) {
+    if (k > 0) {
+      h = (N >> k) / 2;
+      grid = grid_for(c, h);
+      Fe* nx = c->work[(k + 1) & 1].fe();
+      const Fe rr = r;
+      launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, [&] {
+        zk::k_sc_round<F, false><<<grid, zk::kBlock, 0, c->stream>>>(cur, nx, h, rr, c->partials.fe());
+      });
+      cur = nx;
+      read_sums<F, 2>(c, grid, false, s);
+    }
+    rp[2 * k] = s[0];
+    rp[2 * k + 1] = s[1];
+    absorb<F>(tr, s, 2);
+    r = challenge<F>(tr);
+  }
+}
+
+// MultilinearPoly::evaluate on device: n folds at bit 0, ping-pong workspaces
+template <class F>
+Fe mle_evaluate_device(zk_ctx* c, const Fe* dX, uint32_t n, const std::vector<Fe>& pt) {
+  const uint64_t N = (uint64_t)1 << n;
+  Fe res;
+  if (n == 0) {
+    HIPCK(hipMemcpyAsync(&res, dX, 32, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    return res;
+  }
+  c->work[0].ensure(std::max<uint64_t>(N / 2, 1) * 32);
+  c->work[1].ensure(std::max<uint64_t>(N / 4, 1) * 32);
+  const Fe* cur = dX;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t half = N >> (i + 1);
+    Fe* nx = c->work[i & 1].fe();
+    const uint32_t grid = grid_for(c, half);
+    const Fe r = pt[i];
+    const uint32_t s = n - 1 - i;  // bit 0 of the current (n-i)-variable table
+    launch(c, ZK_K_FOLD, 96.0 * half, (double)half, [&] {
+      zk::k_fold<F><<<grid, zk::kBlock, 0, c->stream>>>(cur, nx, half, s, r);
+    });
+    cur = nx;
+  }
+  HIPCK(hipMemcpyAsync(&res, cur, 32, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  return res;
+}
+
+// ---------------------------------------------------------------------------
+// host <-> device staging with representation conversion
+// ---------------------------------------------------------------------------
+template <class F>
+void upload(zk_ctx* c, zk_repr repr, const zk_fe* host, size_t n, Fe* dev) {
+  if (n == 0) return;
+  HIPCK(hipMemcpyAsync(dev, host, n * 32, hipMemcpyHostToDevice, c->stream));
+  HIPCK(hipMemsetAsync(d_flag(c), 0, 4, c->stream));
+  const uint32_t grid = grid_for(c, n);
+  launch(c, ZK_K_CONVERT, 32.0 * n, 0,
+         [&] { zk::k_check_canonical<F><<<grid, zk::kBlock, 0, c->stream>>>(dev, n, d_flag(c)); });
+  if (repr == ZK_REPR_CANONICAL)
+    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n,
+           [&] { zk::k_convert<F, true><<<grid, zk::kBlock, 0, c->stream>>>(dev, dev, n); });
+  uint32_t bad = 0;
+  HIPCK(hipMemcpyAsync(&bad, d_flag(c), 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  require(bad == 0, "field element >= modulus in input table");
+}
+template <class F>
+void download(zk_ctx* c, zk_repr repr, const Fe* dev, size_t n, zk_fe* host) {
+  if (n == 0) return;
+  if (repr == ZK_REPR_CANONICAL) {
+    c->work[1].ensure(std::max(c->work[1].bytes, n * 32));
+    Fe* tmp = c->work[1].fe();
+    const uint32_t grid = grid_for(c, n);
+    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n,
+           [&] { zk::k_convert<F, false><<<grid, zk::kBlock, 0, c->stream>>>(dev, tmp, n); });
+    dev = tmp;
+  }
+  HIPCK(hipMemcpyAsync(host, dev, n * 32, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+}
+
+// canonical table bytes for the plain-prove transcript (fq_vec_to_bytes)
+template <class F>
+std::vector<uint8_t> table_bytes_from_device(zk_ctx* c, const Fe* dev, size_t n) {
+  std::vector<uint8_t> b(n * 32);
+  download<F>(c, ZK_REPR_CANONICAL, dev, n, reinterpret_cast<zk_fe*>(b.data()));
+  return b;
+}
+
+bool pow2_ok(uint32_t nvars) { return nvars < 40; }
+
+template <class F>
+void emit_gkr(zk_repr repr, const GkrOut& g, uint32_t n, zk_fe* out_coeffs, uint8_t* out_ncoeffs,
+              zk_fe* out_challenges) {
+  for (uint32_t k = 0; k < n; ++k) {
+    out_ncoeffs[k] = g.ncoeffs[k];
+    for (int i = 0; i < 3; ++i) out_coeffs[3 * k + i] = out_repr<F>(repr, g.coeffs[3 * k + i]);
+    out_challenges[k] = out_repr<F>(repr, g.challenges[k]);
+  }
+}
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+uint32_t zk_abi_version(void) { return ZK_ABI_VERSION; }
+const char* zk_last_error(void) { return g_last_error.c_str(); }
+
+int zk_ctx_create(int device, zk_ctx** out) {
+  return guarded([&] {
+    require(out != nullptr, "out is null");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+      (void)hipGetLastError();
+      fail(ZK_EDEVICE, "no HIP device available (the prover has no CPU fallback)");
+    }
+    require(device >= 0 && device < ndev, "device index out of range");
+    hipDeviceProp_t prop;
+    HIPCK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+      fail(ZK_EDEVICE, std::string("kernels are built for gfx950, device is ") + prop.gcnArchName);
+    auto* c = new zk_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount;
+    try {
+      bind(c);
+      HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      c->small.ensure(kSmallBytes);
+      HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), 4096, hipHostMallocDefault));
+    } catch (...) {
+      zk_ctx_destroy(c);
+      throw;
+    }
+    *out = c;
+  });
+}
+
+void zk_ctx_destroy(zk_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  for (auto& p : c->pending) c->ev_free.push_back({p.a, p.b});
+  for (auto& e : c->ev_free) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  c->work[0].release();
+  c->work[1].release();
+  c->input.release();
+  c->partials.release();
+  c->small.release();
+  if (c->h_red) (void)hipHostFree(c->h_red);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int zk_ctx_set_timing(zk_ctx* c, int enable) {
+  return guarded([&] {
+    require(c, "ctx is null");
+    c->timing = enable != 0;
+  });
+}
+int zk_ctx_get_stats(const zk_ctx* c, zk_stats* out) {
+  return guarded([&] {
+    require(c && out, "null argument");
+    *out = c->stats;
+  });
+}
+int zk_ctx_reset_stats(zk_ctx* c) {
+  return guarded([&] {
+    require(c, "ctx is null");
+    c->stats = zk_stats{};
+  });
+}
+
+// ---- transcript ----
+zk_transcript* zk_transcript_new(void) { return new (std::nothrow) zk_transcript(); }
+zk_transcript* zk_transcript_clone(const zk_transcript* t) {
+  return t ? new (std::nothrow) zk_transcript(*t) : nullptr;
+}
+void zk_transcript_free(zk_transcript* t) { delete t; }
+int zk_transcript_append(zk_transcript* t, const uint8_t* data, size_t len) {
+  return guarded([&] {
+    require(t && (data || len == 0), "null argument");
+    t->h.update(data, len);
+  });
+}
+int zk_transcript_get_random_challenge(zk_transcript* t, zk_field field, zk_repr repr, zk_fe* out) {
+  return guarded([&] {
+    require(t && out, "null argument");
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      *out = out_repr<F>(repr, challenge<F>(t));
+    });
+  });
+}
+int zk_fe_vec_to_bytes(zk_field field, zk_repr repr, const zk_fe* v, size_t n, uint8_t* out) {
+  return guarded([&] {
+    require((v && out) || n == 0, "null argument");
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      for (size_t i = 0; i < n; ++i) canon_bytes<F>(in_mont<F>(repr, v[i]), out + 32 * i);
+    });
+  });
+}
+
+// ---- MultilinearPoly ----
+int zk_mle_partial_evaluate(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                            uint32_t bit, const zk_fe* value, zk_fe* out) {
+  return guarded([&] {
+    require(c && evals && value && out, "null argument");
+    require(pow2_ok(nvars), "table too large");
+    require(nvars >= 1, "partial_evaluate of a 0-variable polynomial (pair_points underflow panics)");
+    require(bit < nvars, "bit >= num_of_vars (pair_points underflow panics)");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t N = (uint64_t)1 << nvars, half = N / 2;
+      const Fe r = in_mont<F>(repr, *value);
+      c->input.ensure(N * 32);
+      upload<F>(c, repr, evals, N, c->input.fe());
+      c->work[0].ensure(half * 32);
+      const uint32_t grid = grid_for(c, half);
+      const uint32_t s = nvars - 1 - bit;
+      launch(c, ZK_K_FOLD, 96.0 * half, (double)half, [&] {
+        zk::k_fold<F><<<grid, zk::kBlock, 0, c->stream>>>(c->input.fe(), c->work[0].fe(), half, s, r);
+      });
+      download<F>(c, repr, c->work[0].fe(), half, out);
+    });
+  });
+}
+
+int zk_mle_evaluate(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                    const zk_fe* point, uint32_t npoint, zk_fe* out) {
+  return guarded([&] {
+    require(c && evals && out && (point || npoint == 0), "null argument");
+    require(pow2_ok(nvars), "table too large");
+    require(npoint == nvars, "Invalid number of values");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t N = (uint64_t)1 << nvars;
+      std::vector<Fe> pt(nvars);
+      for (uint32_t i = 0; i < nvars; ++i) pt[i] = in_mont<F>(repr, point[i]);
+      c->input.ensure(N * 32);
+      upload<F>(c, repr, evals, N, c->input.fe());
+      *out = out_repr<F>(repr, mle_evaluate_device<F>(c, c->input.fe(), nvars, pt));
+    });
+  });
+}
+
+// ---- sum-check ----
+int zk_sumcheck_prove(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                      zk_fe* out_round_polys, zk_fe* out_claimed_sum) {
+  return guarded([&] {
+    require(c && evals && out_claimed_sum && (out_round_polys || nvars == 0), "null argument");
+    require(pow2_ok(nvars), "table too large");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t N = (uint64_t)1 << nvars;
+      c->input.ensure(N * 32);
+      upload<F>(c, repr, evals, N, c->input.fe());
+      std::vector<uint8_t> bytes;
+      const uint8_t* tb = reinterpret_cast<const uint8_t*>(evals);  // canonical host bytes == fq_vec_to_bytes
+      if (repr == ZK_REPR_MONTGOMERY) {
+        bytes = table_bytes_from_device<F>(c, c->input.fe(), N);
+        tb = bytes.data();
+      }
+      zk_transcript tr;
+      std::vector<Fe> rp(2 * (size_t)nvars + 1);
+      Fe claimed;
+      sc_prove_device<F>(c, c->input.fe(), nvars, &tr, tb, N * 32, rp.data(), claimed);
+      for (size_t i = 0; i < 2 * (size_t)nvars; ++i) out_round_polys[i] = out_repr<F>(repr, rp[i]);
+      *out_claimed_sum = out_repr<F>(repr, claimed);
+    });
+  });
+}
+
+int zk_sumcheck_verify(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                       const zk_fe* round_polys, uint32_t nrounds, uint32_t poly_len, const zk_fe* claimed_sum,
+                       int* out_verified) {
+  return guarded([&] {
+    require(c && evals && claimed_sum && out_verified && (round_polys || nrounds == 0), "null argument");
+    require(pow2_ok(nvars), "table too large");
+    // MultilinearPoly::new(poly.to_vec()) panics on non-power-of-two length (:64)
+    require(nrounds == 0 || (poly_len != 0 && (poly_len & (poly_len - 1)) == 0), "Invalid evaluations");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t N = (uint64_t)1 << nvars;
+      c->input.ensure(N * 32);
+      upload<F>(c, repr, evals, N, c->input.fe());
+      zk_transcript tr;
+      if (repr == ZK_REPR_MONTGOMERY) {
+        auto b = table_bytes_from_device<F>(c, c->input.fe(), N);
+        tr.h.update(b.data(), b.size());
+      } else {
+        tr.h.update(reinterpret_cast<const uint8_t*>(evals), N * 32);
+      }
+      Fe expected = in_mont<F>(repr, *claimed_sum);
+      absorb<F>(&tr, &expected, 1);
+      std::vector<Fe> chal, pv(poly_len ? poly_len : 1);
+      uint32_t tables_left = nvars;  // the redundant fold (:76) panics once exhausted
+      for (uint32_t k = 0; k < nrounds; ++k) {
+        Fe s = zk::fe_zero<F>();
+        for (uint32_t i = 0; i < poly_len; ++i) {
+          pv[i] = in_mont<F>(repr, round_polys[(size_t)k * poly_len + i]);
+          s = zk::fe_add<F>(s, pv[i]);
+        }
+        if (!zk::fe_eq<F>(s, expected)) {  // :66-68
+          *out_verified = 0;
+          return;
+        }
+        require(poly_len >= 2, "index out of bounds: poly.evaluation[1]");
+        absorb<F>(&tr, pv.data(), poly_len);
+        const Fe r = challenge<F>(&tr);
+        expected = zk::fe_add<F>(pv[0], zk::fe_mul<F>(r, zk::fe_sub<F>(pv[1], pv[0])));  // :73-74
+        require(tables_left > 0, "partial_evaluate of a 0-variable polynomial (pair_points underflow panics)");
+        --tables_left;
+        chal.push_back(r);
+      }
+      require(chal.size() == nvars, "Invalid number of values");  // evaluate() :80-82
+      const Fe v = mle_evaluate_device<F>(c, c->input.fe(), nvars, chal);
+      *out_verified = zk::fe_eq<F>(expected, v) ? 1 : 0;
+    });
+  });
+}
+
+int zk_gkr_sumcheck_prove(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* const tables[4], uint32_t nvars,
+                          const zk_fe* claimed_sum, zk_transcript* transcript, zk_fe* out_coeffs,
+                          uint8_t* out_ncoeffs, zk_fe* out_challenges, zk_fe* out_claimed_sum) {
+  return guarded([&] {
+    require(c && tables && claimed_sum && transcript && out_claimed_sum, "null argument");
+    require(nvars == 0 || (out_coeffs && out_ncoeffs && out_challenges), "null output");
+    for (int t = 0; t < 4; ++t) require(tables[t] != nullptr, "null table");
+    require(pow2_ok(nvars), "table too large");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const Fe cs = in_mont<F>(repr, *claimed_sum);
+      const uint64_t N = (uint64_t)1 << nvars;
+      c->input.ensure(4 * N * 32);
+      const Fe* dT[4];
+      for (int t = 0; t < 4; ++t) {
+        upload<F>(c, repr, tables[t], N, c->input.fe(t * N));
+        dT[t] = c->input.fe(t * N);
+      }
+      GkrOut g;
+      gkr_prove_device<F>(c, dT, nvars, false, transcript, g);
+      emit_gkr<F>(repr, g, nvars, out_coeffs, out_ncoeffs, out_challenges);
+      *out_claimed_sum = out_repr<F>(repr, cs);  // carried through (:110-114)
+    });
+  });
+}
+
+int zk_gkr_sumcheck_verify(zk_field field, zk_repr repr, const zk_fe* coeffs, const uint8_t* ncoeffs,
+                           uint32_t nrounds, const zk_fe* claimed_sum, zk_transcript* transcript, int* out_verified,
+                           zk_fe* out_final_claimed_sum, zk_fe* out_challenges) {
+  return guarded([&] {
+    require(claimed_sum && transcript && out_verified && out_final_claimed_sum && out_challenges, "null argument");
+    require(nrounds == 0 || (coeffs && ncoeffs), "null argument");
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      using namespace zk;
+      Fe claim = in_mont<F>(repr, *claimed_sum);
+      const Fe zero = fe_zero<F>(), one = fe_one<F>();
+      for (uint32_t k = 0; k < nrounds; ++k) {
+        require(ncoeffs[k] <= 3, "round polynomial has more than 3 coefficients");
+        Fe cf[3];
+        const int m = ncoeffs[k];
+        for (int i = 0; i < m; ++i) cf[i] = in_mont<F>(repr, coeffs[3 * k + i]);
+        // UnivariatePoly::evaluate (univariate_polynomial_dense.rs:20-26)
+        auto eval = [&](const Fe& x) {
+          Fe s = zero, xp = one;
+          for (int i = 0; i < m; ++i) {
+            s = fe_add<F>(s, fe_mul<F>(cf[i], xp));
+            xp = fe_mul<F>(xp, x);
+          }
+          return s;
+        };
+        if (!fe_eq<F>(fe_add<F>(eval(zero), eval(one)), claim)) {  // :128-134
+          *out_verified = 0;
+          *out_final_claimed_sum = out_repr<F>(repr, zero);
+          out_challenges[0] = out_repr<F>(repr, zero);
+          return;
+        }
+        absorb<F>(transcript, cf, (size_t)m);
+        const Fe r = challenge<F>(transcript);
+        out_challenges[k] = out_repr<F>(repr, r);
+        claim = eval(r);
+      }
+      *out_verified = 1;
+      *out_final_claimed_sum = out_repr<F>(repr, claim);
+    });
+  });
+}
+
+// ---- device-resident API ----
+int zk_dev_alloc(zk_ctx* c, size_t bytes, void** out) {
+  return guarded([&] {
+    require(c && out, "null argument");
+    bind(c);
+    *out = nullptr;
+    if (hipMalloc(out, bytes ? bytes : 1) != hipSuccess) {
+      (void)hipGetLastError();
+      *out = nullptr;
+      fail(ZK_ENOMEM, "hipMalloc failed");
+    }
+  });
+}
+int zk_dev_free(zk_ctx* c, void* p) {
+  return guarded([&] {
+    require(c, "null ctx");
+    bind(c);
+    if (p) HIPCK(hipFree(p));
+  });
+}
+int zk_dev_upload(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* host, size_t n, void* dev) {
+  return guarded([&] {
+    require(c && (n == 0 || (host && dev)), "null argument");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      upload<F>(c, repr, host, n, reinterpret_cast<Fe*>(dev));
+    });
+  });
+}
+int zk_dev_download(zk_ctx* c, zk_field field, zk_repr repr, const void* dev, size_t n, zk_fe* host) {
+  return guarded([&] {
+    require(c && (n == 0 || (host && dev)), "null argument");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      download<F>(c, repr, reinterpret_cast<const Fe*>(dev), n, host);
+    });
+  });
+}
+int zk_dev_synth_fill(zk_ctx* c, zk_field field, void* dev, uint64_t count, uint64_t seed, uint32_t table,
+                      uint64_t index0, uint64_t stride) {
+  return guarded([&] {
+    require(c && (dev || count == 0), "null argument");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t key = zk::splitmix64(zk::splitmix64(seed) + table);
+      const uint32_t grid = grid_for(c, count);
+      launch(c, ZK_K_SYNTH, 32.0 * count, (double)count, [&] {
+        zk::k_synth<F><<<grid, zk::kBlock, 0, c->stream>>>(reinterpret_cast<Fe*>(dev), count, key, index0, stride);
+      });
+      sync(c);
+    });
+  });
+}
+int zk_dev_mle_partial_evaluate(zk_ctx* c, zk_field field, const void* d_in, uint32_t nvars, uint32_t bit,
+                                zk_repr repr, const zk_fe* value, void* d_out) {
+  return guarded([&] {
+    require(c && d_in && d_out && value, "null argument");
+    require(nvars >= 1 && bit < nvars, "pair_points underflow panics");
+    require(d_in != d_out, "d_out may not alias d_in");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const Fe r = in_mont<F>(repr, *value);
+      const uint64_t half = (uint64_t)1 << (nvars - 1);
+      const uint32_t grid = grid_for(c, half);
+      const uint32_t s = nvars - 1 - bit;
+      launch(c, ZK_K_FOLD, 96.0 * half, (double)half, [&] {
+        zk::k_fold<F><<<grid, zk::kBlock, 0, c->stream>>>(reinterpret_cast<const Fe*>(d_in),
+                                                          reinterpret_cast<Fe*>(d_out), half, s, r);
+      });
+      sync(c);
+    });
+  });
+}
+int zk_dev_gkr_sumcheck_prove(zk_ctx* c, zk_field field, const void* const d_tables[4], uint32_t nvars,
+                              zk_repr repr, const zk_fe* claimed_sum, zk_transcript* transcript, zk_fe* out_coeffs,
+                              uint8_t* out_ncoeffs, zk_fe* out_challenges) {
+  return guarded([&] {
+    require(c && d_tables && transcript && claimed_sum, "null argument");
+    require(nvars == 0 || (out_coeffs && out_ncoeffs && out_challenges), "null output");
+    for (int t = 0; t < 4; ++t) require(d_tables[t] != nullptr, "null table");
+    require(pow2_ok(nvars), "table too large");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      (void)in_mont<F>(repr, *claimed_sum);
+      const Fe* dT[4];
+      for (int t = 0; t < 4; ++t) dT[t] = reinterpret_cast<const Fe*>(d_tables[t]);
+      GkrOut g;
+      gkr_prove_device<F>(c, dT, nvars, false, transcript, g);
+      emit_gkr<F>(repr, g, nvars, out_coeffs, out_ncoeffs, out_challenges);
+    });
+  });
+}
+
+// ---- multi-GPU ----
+int zk_ctx_attach_host_comm(zk_ctx* c, int rank, int world, zk_allreduce_u64_fn allreduce, zk_allgather_fn allgather,
+                            void* user) {
+  return guarded([&] {
+    require(c && allreduce && allgather, "null argument");
+    require(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
+    require(rank >= 0 && rank < world, "rank out of range");
+    if (c->nccl) {
+      (void)ncclCommDestroy(c->nccl);
+      c->nccl = nullptr;
+    }
+    c->rank = rank;
+    c->world = world;
+    c->comm = COMM_HOST;
+    c->ar = allreduce;
+    c->ag = allgather;
+    c->user = user;
+  });
+}
+int zk_comm_get_unique_id(uint8_t out[128]) {
+  return guarded([&] {
+    require(out, "null argument");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCLCK(ncclGetUniqueId(&id));
+    memcpy(out, &id, 128);
+  });
+}
+int zk_ctx_attach_rccl(zk_ctx* c, int rank, int world, const uint8_t unique_id[128]) {
+  return guarded([&] {
+    require(c && unique_id, "null argument");
+    require(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
+    require(rank >= 0 && rank < world, "rank out of range");
+    bind(c);
+    if (c->nccl) {
+      (void)ncclCommDestroy(c->nccl);
+      c->nccl = nullptr;
+    }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, 128);
+    NCCLCK(ncclCommInitRank(&c->nccl, world, id, rank));
+    c->rank = rank;
+    c->world = world;
+    c->comm = COMM_RCCL;
+  });
+}
+int zk_ctx_detach_comm(zk_ctx* c) {
+  return guarded([&] {
+    require(c, "null ctx");
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    c->nccl = nullptr;
+    c->rank = 0;
+    c->world = 1;
+    c->comm = COMM_NONE;
+  });
+}
+int zk_dev_gkr_sumcheck_prove_sharded(zk_ctx* c, zk_field field, const void* const d_local_tables[4],
+                                      uint32_t nvars_local, zk_repr repr, const zk_fe* claimed_sum,
+                                      zk_transcript* transcript, zk_fe* out_coeffs, uint8_t* out_ncoeffs,
+                                      zk_fe* out_challenges) {
+  return guarded([&] {
+    require(c && d_local_tables && transcript && claimed_sum && out_coeffs && out_ncoeffs && out_challenges,
+            "null argument");
+    for (int t = 0; t < 4; ++t) require(d_local_tables[t] != nullptr, "null table");
+    require(pow2_ok(nvars_local), "table too large");
+    require(c->world == 1 || c->comm != COMM_NONE, "no communicator attached");
+    require(1024 + 128 + (size_t)c->world * 256 <= kSmallBytes, "world too large for the gather buffer");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      (void)in_mont<F>(repr, *claimed_sum);
+      const Fe* dT[4];
+      for (int t = 0; t < 4; ++t) dT[t] = reinterpret_cast<const Fe*>(d_local_tables[t]);
+      GkrOut g;
+      gkr_prove_device<F>(c, dT, nvars_local, true, transcript, g);
+      uint32_t lg = 0;
+      while ((1 << lg) < c->world) ++lg;
+      emit_gkr<F>(repr, g, nvars_local + lg, out_coeffs, out_ncoeffs, out_challenges);
+    });
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,101 @@
+"""ctypes binding of libzksumcheck.so (include/zk_sumcheck.h).
+
+The library is the product: HIP kernels for gfx950 plus the C++ host
+orchestration. Loading it never falls back to anything else — if the shared
+object is missing this module raises, and creating a context on a machine
+without a gfx950 GPU fails with ZK_EDEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libzksumcheck.so")
+PKG_ROOT = os.path.dirname(_HERE)
+
+ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
+ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
+KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth"]
+
+
+class ZkError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class ZkStats(C.Structure):
+    _fields_ = [
+        ("launches", C.c_uint64 * 7),
+        ("kernel_ms", C.c_double * 7),
+        ("alg_bytes", C.c_double * 7),
+        ("field_muls", C.c_double * 7),
+        ("host_syncs", C.c_uint64),
+        ("collectives", C.c_uint64),
+    ]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
+
+# name -> (restype, argtypes); every symbol declared in include/zk_sumcheck.h
+P, I, U32, U64, SZ = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64, C.c_size_t
+SIGNATURES = {
+    "zk_abi_version": (U32, []),
+    "zk_last_error": (C.c_char_p, []),
+    "zk_ctx_create": (I, [I, C.POINTER(C.c_void_p)]),
+    "zk_ctx_destroy": (None, [P]),
+    "zk_ctx_set_timing": (I, [P, I]),
+    "zk_ctx_get_stats": (I, [P, C.POINTER(ZkStats)]),
+    "zk_ctx_reset_stats": (I, [P]),
+    "zk_transcript_new": (P, []),
+    "zk_transcript_clone": (P, [P]),
+    "zk_transcript_free": (None, [P]),
+    "zk_transcript_append": (I, [P, P, SZ]),
+    "zk_transcript_get_random_challenge": (I, [P, I, I, P]),
+    "zk_fe_vec_to_bytes": (I, [I, I, P, SZ, P]),
+    "zk_mle_partial_evaluate": (I, [P, I, I, P, U32, U32, P, P]),
+    "zk_mle_evaluate": (I, [P, I, I, P, U32, P, U32, P]),
+    "zk_sumcheck_prove": (I, [P, I, I, P, U32, P, P]),
+    "zk_sumcheck_verify": (I, [P, I, I, P, U32, P, U32, U32, P, C.POINTER(C.c_int)]),
+    "zk_gkr_sumcheck_prove": (I, [P, I, I, P, U32, P, P, P, P, P, P]),
+    "zk_gkr_sumcheck_verify": (I, [I, I, P, P, U32, P, P, C.POINTER(C.c_int), P, P]),
+    "zk_dev_alloc": (I, [P, SZ, C.POINTER(C.c_void_p)]),
+    "zk_dev_free": (I, [P, P]),
+    "zk_dev_upload": (I, [P, I, I, P, SZ, P]),
+    "zk_dev_download": (I, [P, I, I, P, SZ, P]),
+    "zk_dev_synth_fill": (I, [P, I, P, U64, U64, U32, U64, U64]),
+    "zk_dev_mle_partial_evaluate": (I, [P, I, P, U32, U32, I, P, P]),
+    "zk_dev_gkr_sumcheck_prove": (I, [P, I, P, U32, I, P, P, P, P, P]),
+    "zk_ctx_attach_host_comm": (I, [P, I, I, ALLREDUCE_FN, ALLGATHER_FN, P]),
+    "zk_comm_get_unique_id": (I, [P]),
+    "zk_ctx_attach_rccl": (I, [P, I, I, P]),
+    "zk_ctx_detach_comm": (I, [P]),
+    "zk_dev_gkr_sumcheck_prove_sharded": (I, [P, I, P, U32, I, P, P, P, P, P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
+                "(or __graft_entry__.build()); the prover has no CPU fallback"
+            )
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(code: int) -> None:
+    if code != ZK_OK:
+        raise ZkError(code, lib().zk_last_error().decode(errors="replace"))

@@ -1,0 +1,142 @@
+"""Device context and device-resident tables (zk_ctx / zk_dev_* of the C ABI)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import KERNEL_KINDS, check, lib
+from .elems import as_limbs, ptr, to_ints
+
+REPR_CANONICAL, REPR_MONTGOMERY = 0, 1
+
+
+class Context:
+    """One HIP device + stream + workspace (+ optional communicator)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().zk_ctx_create(int(device), C.byref(h)))
+        self.h = h
+        self.device = device
+        self._callbacks = None  # keep ctypes callbacks alive while attached
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().zk_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- stats ----
+    def set_timing(self, enable: bool) -> None:
+        check(lib().zk_ctx_set_timing(self.h, int(bool(enable))))
+
+    def reset_stats(self) -> None:
+        check(lib().zk_ctx_reset_stats(self.h))
+
+    def stats(self) -> dict:
+        s = _lib.ZkStats()
+        check(lib().zk_ctx_get_stats(self.h, C.byref(s)))
+        return {
+            "kernels": {
+                k: {
+                    "launches": int(s.launches[i]),
+                    "ms": float(s.kernel_ms[i]),
+                    "alg_bytes": float(s.alg_bytes[i]),
+                    "field_muls": float(s.field_muls[i]),
+                }
+                for i, k in enumerate(KERNEL_KINDS)
+            },
+            "host_syncs": int(s.host_syncs),
+            "collectives": int(s.collectives),
+        }
+
+    # ---- device tables ----
+    def alloc(self, field: int, count: int) -> "DeviceTable":
+        return DeviceTable(self, field, count)
+
+    def upload(self, field: int, values, repr: int = REPR_CANONICAL) -> "DeviceTable":
+        a = as_limbs(values)
+        t = DeviceTable(self, field, a.shape[0])
+        check(lib().zk_dev_upload(self.h, field, repr, ptr(a), a.shape[0], t.ptr))
+        return t
+
+    def synth(self, field: int, count: int, seed: int, table: int, index0: int = 0, stride: int = 1) -> "DeviceTable":
+        t = DeviceTable(self, field, count)
+        check(lib().zk_dev_synth_fill(self.h, field, t.ptr, count, seed, table, index0, stride))
+        return t
+
+    # ---- communicators ----
+    def attach_rccl(self, rank: int, world: int, unique_id: bytes) -> None:
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        check(lib().zk_ctx_attach_rccl(self.h, rank, world, buf))
+
+    def attach_host_comm(self, rank: int, world: int, allreduce, allgather) -> None:
+        """allreduce(np.ndarray[uint64]) -> None (in-place SUM);
+        allgather(bytes) -> bytes (rank-ordered concatenation)."""
+
+        def _ar(user, data, count):
+            try:
+                arr = np.ctypeslib.as_array(data, shape=(count,))
+                allreduce(arr)
+                return 0
+            except Exception:  # the C side turns this into ZK_ECOMM
+                return 1
+
+        def _ag(user, send, recv, nbytes):
+            try:
+                mine = C.string_at(send, nbytes)
+                allb = allgather(mine)
+                C.memmove(recv, allb, len(allb))
+                return 0
+            except Exception:
+                return 1
+
+        cbs = (_lib.ALLREDUCE_FN(_ar), _lib.ALLGATHER_FN(_ag))
+        check(lib().zk_ctx_attach_host_comm(self.h, rank, world, cbs[0], cbs[1], None))
+        self._callbacks = cbs
+
+    def detach_comm(self) -> None:
+        check(lib().zk_ctx_detach_comm(self.h))
+        self._callbacks = None
+
+
+def rccl_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    check(lib().zk_comm_get_unique_id(buf))
+    return bytes(buf)
+
+
+class DeviceTable:
+    """A device buffer of `count` Montgomery field elements (32 B each)."""
+
+    def __init__(self, ctx: Context, field: int, count: int):
+        self.ctx, self.field, self.count = ctx, field, int(count)
+        p = C.c_void_p()
+        check(lib().zk_dev_alloc(ctx.h, max(1, self.count) * 32, C.byref(p)))
+        self.ptr = p
+
+    def free(self) -> None:
+        if getattr(self, "ptr", None) and self.ctx.h:
+            lib().zk_dev_free(self.ctx.h, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def download(self, repr: int = REPR_CANONICAL) -> np.ndarray:
+        out = np.zeros((self.count, 4), np.uint64)
+        check(lib().zk_dev_download(self.ctx.h, self.field, repr, self.ptr, self.count, ptr(out)))
+        return out
+
+    def to_ints(self) -> list[int]:
+        return to_ints(self.download())
