@@ -85,7 +85,8 @@ typedef struct {
   uint64_t host_syncs;           /* device->host round trips */
   uint64_t collectives;          /* all-reduce / all-gather calls */
 } zk_stats;
-int zk_ctx_set_timing(zk_ctx* ctx, int enable);
+int zk_ctx_set_timing(zk_ctx* ctx, int enable);                /* all kinds on / off */
+int zk_ctx_set_timing_mask(zk_ctx* ctx, uint32_t kind_mask);   /* bit k = time ZK_K_k launches */
 int zk_ctx_get_stats(const zk_ctx* ctx, zk_stats* out);
 int zk_ctx_reset_stats(zk_ctx* ctx);
 
@@ -161,16 +162,16 @@ int zk_dev_gkr_sumcheck_prove(zk_ctx* ctx, zk_field field, const void* const d_t
  * per GPU, world a power of two). Rank g holds the sub-cube whose LOW
  * log2(world) index bits equal g: local m <-> global m*world + g. The first
  * nvars_local rounds fold purely locally; each round's partial sums are
- * combined with ONE all-reduce of 24 u64 (three elements split into 32-bit
- * limbs, exact); one all-gather of 4 elements per rank then lets every rank
- * finish the last log2(world) rounds identically. No broadcast is needed:
- * every rank derives the same challenges from the same transcript.
+ * combined with ONE all-reduce of at most 24 u64 (three elements split into
+ * 32-bit limbs, so the u64 sum is exact); a last all-reduce of one-hot slots
+ * gathers the 4 remaining elements of every rank so all ranks finish the last
+ * log2(world) rounds identically. All-reduce (SUM, u64) is the only collective.
+ * No broadcast is needed: every rank derives the same challenges from the
+ * same transcript.
  * ------------------------------------------------------------------------- */
-/* host-memory collectives supplied by the caller (e.g. torch.distributed/gloo) */
-typedef int (*zk_allreduce_u64_fn)(void* user, uint64_t* data, size_t count);          /* in-place SUM */
-typedef int (*zk_allgather_fn)(void* user, const void* send, void* recv, size_t bytes); /* rank-ordered */
-int zk_ctx_attach_host_comm(zk_ctx* ctx, int rank, int world, zk_allreduce_u64_fn allreduce,
-                            zk_allgather_fn allgather, void* user);
+/* host-memory all-reduce supplied by the caller (e.g. torch.distributed/gloo) */
+typedef int (*zk_allreduce_u64_fn)(void* user, uint64_t* data, size_t count); /* in-place SUM, 0 = ok */
+int zk_ctx_attach_host_comm(zk_ctx* ctx, int rank, int world, zk_allreduce_u64_fn allreduce, void* user);
 /* RCCL over xGMI: rank 0 creates the id, every rank passes the same 128 bytes */
 int zk_comm_get_unique_id(uint8_t out[128]);
 int zk_ctx_attach_rccl(zk_ctx* ctx, int rank, int world, const uint8_t unique_id[128]);

@@ -1,0 +1,56 @@
+"""One rank of a sharded GKR sum-check on the GPU (spawned by
+tests/test_gpu_sharded.py; not a test module itself).
+
+env: RANK, WORLD_SIZE, MASTER_PORT, COMM in {host, rccl, none}, FIELD, NLOCAL, OUT
+Rank g proves its low-index-bit shard; rank 0 writes the proof as JSON.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zk-research-implementations_amd"))
+
+
+def main() -> None:
+    import numpy as np
+    import torch.distributed as dist
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+    from zk_amd.dist import TorchAllreduce, rendezvous_rccl, shard_layout
+    from zk_amd.elems import as_limbs, ptr, to_ints
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    comm, field, nloc = os.environ["COMM"], int(os.environ["FIELD"]), int(os.environ["NLOCAL"])
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{os.environ['MASTER_PORT']}", rank=rank,
+                            world_size=world)
+    ctx = zk_amd.Context(0)
+    if comm == "host":
+        ctx.attach_host_comm(rank, world, TorchAllreduce())
+    elif comm == "rccl":
+        rendezvous_rccl(ctx, rank, world)
+    i0, stride = shard_layout(rank, world)
+    tabs = [ctx.synth(field, 1 << nloc, seed=19, table=t, index0=i0, stride=stride) for t in range(4)]
+    n = nloc + world.bit_length() - 1
+    arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
+    coeffs = np.zeros((max(n, 1), 3, 4), np.uint64)
+    nco = np.zeros(max(n, 1), np.uint8)
+    ch = np.zeros((max(n, 1), 4), np.uint64)
+    tr = zk_amd.Transcript(field)
+    check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, nloc, 0, ptr(as_limbs([0])), tr.h, ptr(coeffs),
+                                                  ptr(nco), ptr(ch)))
+    res = {"polys": [[hex(x) for x in to_ints(coeffs[k, : nco[k]])] for k in range(n)],
+           "chal": [hex(x) for x in to_ints(ch[:n])], "collectives": ctx.stats()["collectives"]}
+    with open(os.path.join(os.environ["OUT"], f"rank{rank}.json"), "w") as fh:
+        json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

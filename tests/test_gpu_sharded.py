@@ -1,0 +1,78 @@
+"""Sharded (multi-rank) GKR sum-check on the GPU through the C ABI.
+
+Ranks are separate processes sharing the box's single GPU; their round sums
+meet through the host all-reduce callback over gloo (RCCL refuses two ranks
+on one device). The RCCL data path itself runs at world 1 with
+ZK_FORCE_COLLECTIVES=1, which routes every round through ncclAllReduce and
+the publish kernel. Every rank's proof must equal the oracle's single-process
+proof over the full tables.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+import coracle as co
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "sharded_worker.py")
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world: int, comm: str, field: int, nloc: int, out: str, extra_env=None) -> list[dict]:
+    port = _free_port()
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), MASTER_PORT=str(port), COMM=comm,
+                   FIELD=str(field), NLOCAL=str(nloc), OUT=out, MASTER_ADDR="127.0.0.1", **(extra_env or {}))
+        procs.append(subprocess.Popen([sys.executable, WORKER], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
+    logs = []
+    for p in procs:
+        o, _ = p.communicate(timeout=240)
+        logs.append(o.decode(errors="replace"))
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    res = []
+    for rank in range(world):
+        with open(os.path.join(out, f"rank{rank}.json")) as fh:
+            res.append(json.load(fh))
+    return res
+
+
+def _oracle(field: int, n: int) -> dict:
+    tabs = [co.synth(field, 19, t, 0, 1 << n) for t in range(4)]
+    polys, chal = co.gkr_prove(field, tabs, co.Transcript())
+    return {"polys": [[hex(x) for x in p] for p in polys], "chal": [hex(x) for x in chal]}
+
+
+@pytest.mark.parametrize("world,nloc,field", [(2, 12, 0), (4, 9, 2), (2, 0, 1)])
+def test_host_comm_ranks_match_single_process(tmp_path, world, nloc, field):
+    res = _run(world, "host", field, nloc, str(tmp_path))
+    want = _oracle(field, nloc + world.bit_length() - 1)
+    for rank, r in enumerate(res):
+        assert {"polys": r["polys"], "chal": r["chal"]} == want, f"rank {rank}"
+        assert r["collectives"] == nloc + 1  # one all-reduce per local round + the tail gather
+
+
+def test_world1_without_comm(tmp_path):
+    res = _run(1, "none", 0, 13, str(tmp_path))
+    assert {"polys": res[0]["polys"], "chal": res[0]["chal"]} == _oracle(0, 13)
+    assert res[0]["collectives"] == 0
+
+
+def test_rccl_data_path_forced_at_world1(tmp_path):
+    res = _run(1, "rccl", 0, 14, str(tmp_path), {"ZK_FORCE_COLLECTIVES": "1"})
+    assert {"polys": res[0]["polys"], "chal": res[0]["chal"]} == _oracle(0, 14)
+    assert res[0]["collectives"] == 14  # every round went through ncclAllReduce

@@ -39,56 +39,217 @@ __device__ __forceinline__ Fe at2(const Fe& lo, const Fe& hi) {
   return fe_sub<F>(fe_dbl<F>(hi), lo);
 }
 
-// Sum K field elements over the workgroup; thread 0..K-1 write block partial k.
+// Where a round kernel's K partial sums go. Every block publishes its
+// partial with write-through (sc1) 8-byte stores, drains them, and one lane
+// bumps an agent-scope counter; the block whose add returns gridDim-1 reads
+// all partials back with sc1 loads (MI355X_MICROARCH.md "Valid forms", first
+// row of the sc1 hand-off table: no release/acquire fence, so the dirty L2
+// full of freshly folded table lines is never written back mid-kernel). It
+// writes the K totals limb-split (one u64 per 32-bit limb — the form the
+// multi-GPU all-reduce sums exactly) to dev_out and/or pinned host memory and
+// raises host_flag = tag with a system-scope release; the host spins on that
+// flag instead of synchronising the stream.
+struct RoundSink {
+  Fe* partials;         // [gridDim.x][4]: one 128-B slot per block
+  uint32_t* counter;    // zero at launch; the last block resets it
+  uint64_t* dev_out;    // K*8 u64 in device memory, or null
+  uint64_t* host_out;   // K*8 u64 in pinned host memory, or null
+  uint32_t* host_flag;  // pinned host word, or null
+  uint32_t tag;
+};
+
+__device__ __forceinline__ void st_fe_sc1(Fe* p, uint64_t i, const Fe& x) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p + i);
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+    __hip_atomic_store(q + w, (uint64_t)x.v[2 * w] | ((uint64_t)x.v[2 * w + 1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Fe ld_fe_sc1(Fe* p, uint64_t i) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p + i);
+  Fe x;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint64_t v = __hip_atomic_load(q + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x.v[2 * w] = (uint32_t)v;
+    x.v[2 * w + 1] = (uint32_t)(v >> 32);
+  }
+  return x;
+}
+
+// Block-level sums use plain 288-bit integer adds (9 words, no modular
+// reduction per step): 256 values < p sum to < 2^264. One reduction mod p at
+// the end (lo256 mod p + hi * 2^256 mod p).
+struct W9 {
+  uint32_t w[9];
+};
+__device__ __forceinline__ void w9_add(W9& a, const W9& b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a.w[i] = addc32(a.w[i], b.w[i], c, &c);
+}
+template <class F>
+__device__ __forceinline__ Fe w9_reduce(const W9& a) {
+  Fe lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) lo.v[i] = a.w[i];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) lo = fe_reduce_once<F>(lo);  // 2^256 < 6p
+  if (a.w[8] == 0) return lo;
+  Fe hi = fe_zero<F>(), r2;
+  hi.v[0] = a.w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r2.v[i] = F::R2[i];
+  return fe_add<F>(lo, fe_mul<F>(hi, r2));  // hi * 2^256 mod p
+}
+
+// sum K elements over the workgroup; the result is valid in threads 0..K-1
 template <class F, int K>
-__device__ __forceinline__ void block_reduce_store(Fe (&acc)[K], Fe* __restrict__ partials) {
-  __shared__ Fe sm[kBlock / 64][K];
+__device__ __forceinline__ Fe block_sum(const Fe (&acc)[K], W9 (&sm)[kBlock / 64][K]) {
+  W9 v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[k].w[i] = acc[k].v[i];
+    v[k].w[8] = 0;
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      Fe o;
+      W9 o;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o.v[i] = __shfl_xor(acc[k].v[i], off, 64);
-      acc[k] = fe_add<F>(acc[k], o);
+      for (int i = 0; i < 9; ++i) o.w[i] = __shfl_xor(v[k].w[i], off, 64);
+      w9_add(v[k], o);
     }
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) sm[wave][k] = acc[k];
+    for (int k = 0; k < K; ++k) sm[wave][k] = v[k];
   }
   __syncthreads();
+  Fe s = fe_zero<F>();
   if (threadIdx.x < K) {
-    Fe s = sm[0][threadIdx.x];
+    W9 t = sm[0][threadIdx.x];
 #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) s = fe_add<F>(s, sm[w][threadIdx.x]);
-    st_fe(partials, (uint64_t)blockIdx.x * K + threadIdx.x, s);
+    for (int w = 1; w < kBlock / 64; ++w) w9_add(t, sm[w][threadIdx.x]);
+    s = w9_reduce<F>(t);
+  }
+  return s;
+}
+
+// final K totals -> limb-split outputs + host flag
+template <int K>
+__device__ __forceinline__ void publish_totals(const Fe& t, const RoundSink& sk) {
+  if (threadIdx.x < K) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (sk.dev_out) sk.dev_out[threadIdx.x * 8 + i] = t.v[i];
+      if (sk.host_out) sk.host_out[threadIdx.x * 8 + i] = t.v[i];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && sk.host_flag) {
+    __threadfence_system();
+    __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <class F, int K>
+__device__ __forceinline__ void block_reduce_finish(Fe (&acc)[K], const RoundSink& sk) {
+  __shared__ W9 sm[kBlock / 64][K];
+  __shared__ uint32_t am_last;
+  const Fe s = block_sum<F, K>(acc, sm);
+  if (gridDim.x == 1) {  // single block: its sum is the total
+    publish_totals<K>(s, sk);
+    return;
+  }
+  if (threadIdx.x < K) st_fe_sc1(sk.partials, (uint64_t)blockIdx.x * 4 + threadIdx.x, s);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains before the signal
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    am_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!am_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+  W9 tot[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) tot[k].w[i] = 0;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kBlock) {
+    Fe x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = ld_fe_sc1(sk.partials, (uint64_t)b * 4 + k);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      W9 y;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) y.w[i] = x[k].v[i];
+      y.w[8] = 0;
+      w9_add(tot[k], y);
+    }
+  }
+  Fe red[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) red[k] = w9_reduce<F>(tot[k]);
+  __syncthreads();  // sm is reused
+  const Fe t = block_sum<F, K>(red, sm);
+  if (threadIdx.x == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  publish_totals<K>(t, sk);
+}
+
+// copy K*8 u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
+__global__ void k_publish(const uint64_t* __restrict__ src, int n, uint64_t* host_out, uint32_t* host_flag,
+                          uint32_t tag) {
+  if (threadIdx.x < n) host_out[threadIdx.x] = src[threadIdx.x];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(host_flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 // ---------------------------------------------------------------------------
 // GKR round 0: e_t = sum_j A_t S_t + M_t P_t for t = 0,1,2 over the input
 // tables (size 2h), X_t = X_lo + t (X_hi - X_lo)  — sum_check_protocol.rs:152-166
-// with composed_polynomial.rs:78-99 (reduce = A*S + M*P). 6 muls / pair.
+// with composed_polynomial.rs:78-99 (reduce = A*S + M*P). 6 unreduced products / pair.
 // ---------------------------------------------------------------------------
+// Two threads per pair: waves alternate between the product A*S (q = 0) and
+// M*P (q = 1), so a thread issues its 4 (round 0) or 8 (fused round) loads at
+// once and keeps register pressure low enough for 4 waves/SIMD.
+__device__ __forceinline__ void pair_slot(uint64_t& j, uint32_t& q, uint64_t& step) {
+  const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  q = (uint32_t)(g >> 6) & 1u;
+  j = ((g >> 7) << 6) | (g & 63);
+  step = (uint64_t)gridDim.x * (kBlock / 2);
+}
+
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_gkr_round0(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                        const Fe* __restrict__ M, const Fe* __restrict__ P,
-                                                       uint64_t h, Fe* __restrict__ partials) {
-  Fe acc[3] = {fe_zero<F>(), fe_zero<F>(), fe_zero<F>()};
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < h; j += stride) {
-    const Fe a0 = ld_fe(A, j), a1 = ld_fe(A, j + h), s0 = ld_fe(S, j), s1 = ld_fe(S, j + h);
-    acc[0] = fe_add<F>(acc[0], fe_mul<F>(a0, s0));
-    acc[1] = fe_add<F>(acc[1], fe_mul<F>(a1, s1));
-    acc[2] = fe_add<F>(acc[2], fe_mul<F>(at2<F>(a0, a1), at2<F>(s0, s1)));
-    const Fe m0 = ld_fe(M, j), m1 = ld_fe(M, j + h), p0 = ld_fe(P, j), p1 = ld_fe(P, j + h);
-    acc[0] = fe_add<F>(acc[0], fe_mul<F>(m0, p0));
-    acc[1] = fe_add<F>(acc[1], fe_mul<F>(m1, p1));
-    acc[2] = fe_add<F>(acc[2], fe_mul<F>(at2<F>(m0, m1), at2<F>(p0, p1)));
+                                                       uint64_t h, RoundSink sink) {
+  // products accumulate unreduced (Wide) and are reduced once per thread
+  Wide w0 = wide_zero<F>(), w1 = wide_zero<F>(), w2 = wide_zero<F>();
+  uint64_t j, step;
+  uint32_t q;
+  pair_slot(j, q, step);
+  const Fe* __restrict__ X = q ? M : A;
+  const Fe* __restrict__ Z = q ? P : S;
+  for (; j < h; j += step) {
+    const Fe x0 = ld_fe(X, j), x1 = ld_fe(X, j + h), z0 = ld_fe(Z, j), z1 = ld_fe(Z, j + h);
+    __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
+    wide_mac<F>(w0, x0, z0);
+    wide_mac<F>(w1, x1, z1);
+    wide_mac<F>(w2, at2<F>(x0, x1), at2<F>(z0, z1));
   }
-  block_reduce_store<F, 3>(acc, partials);
+  Fe acc[3] = {wide_redc<F>(w0), wide_redc<F>(w1), wide_redc<F>(w2)};
+  block_reduce_finish<F, 3>(acc, sink);
 }
 
 // ---------------------------------------------------------------------------
@@ -98,53 +259,86 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round0(const Fe* __restrict__ A,
 // Output pair j needs old j, j+h, j+2h, j+3h: folded lo = old[j] + r(old[j+2h]-old[j]),
 // folded hi = old[j+h] + r(old[j+3h]-old[j+h]). e1 is not computed: the host
 // derives it exactly as s_{k-1}(r_{k-1}) - e0. out must not alias
-// in (the host ping-pongs two workspaces). 12 muls / pair.
+// in (the host ping-pongs two workspaces). 8 reduced muls + 4 unreduced products / pair.
 // ---------------------------------------------------------------------------
+// A/B knobs (defaults are the tuned values): minimum waves per SIMD for the
+// fused round kernel, and whether all loads are forced ahead of the arithmetic.
+#ifndef ZK_ROUND_WAVES
+#define ZK_ROUND_WAVES 1
+#endif
+#ifndef ZK_ROUND_LOADS_FIRST
+#define ZK_ROUND_LOADS_FIRST 1
+#endif
 template <class F>
-__global__ __launch_bounds__(kBlock) void k_gkr_round(const Fe* __restrict__ A, const Fe* __restrict__ S,
+__global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2,
                                                       Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h, Fe r,
-                                                      Fe* __restrict__ partials) {
-  Fe acc[2] = {fe_zero<F>(), fe_zero<F>()};
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < h; j += stride) {
-    Fe a0, a1, s0, s1;
-    {
-      const Fe x0 = ld_fe(A, j), x1 = ld_fe(A, j + h), x2 = ld_fe(A, j + 2 * h), x3 = ld_fe(A, j + 3 * h);
-      a0 = fold1<F>(x0, x2, r);
-      a1 = fold1<F>(x1, x3, r);
-    }
-    {
-      const Fe x0 = ld_fe(S, j), x1 = ld_fe(S, j + h), x2 = ld_fe(S, j + 2 * h), x3 = ld_fe(S, j + 3 * h);
-      s0 = fold1<F>(x0, x2, r);
-      s1 = fold1<F>(x1, x3, r);
-    }
-    st_fe(A2, j, a0);
-    st_fe(A2, j + h, a1);
-    st_fe(S2, j, s0);
-    st_fe(S2, j + h, s1);
-    acc[0] = fe_add<F>(acc[0], fe_mul<F>(a0, s0));
-    acc[1] = fe_add<F>(acc[1], fe_mul<F>(at2<F>(a0, a1), at2<F>(s0, s1)));
-    Fe m0, m1, p0, p1;
-    {
-      const Fe x0 = ld_fe(M, j), x1 = ld_fe(M, j + h), x2 = ld_fe(M, j + 2 * h), x3 = ld_fe(M, j + 3 * h);
-      m0 = fold1<F>(x0, x2, r);
-      m1 = fold1<F>(x1, x3, r);
-    }
-    {
-      const Fe x0 = ld_fe(P, j), x1 = ld_fe(P, j + h), x2 = ld_fe(P, j + 2 * h), x3 = ld_fe(P, j + 3 * h);
-      p0 = fold1<F>(x0, x2, r);
-      p1 = fold1<F>(x1, x3, r);
-    }
-    st_fe(M2, j, m0);
-    st_fe(M2, j + h, m1);
-    st_fe(P2, j, p0);
-    st_fe(P2, j + h, p1);
-    acc[0] = fe_add<F>(acc[0], fe_mul<F>(m0, p0));
-    acc[1] = fe_add<F>(acc[1], fe_mul<F>(at2<F>(m0, m1), at2<F>(p0, p1)));
+                                                      RoundSink sink) {
+  Wide w0 = wide_zero<F>(), w2 = wide_zero<F>();
+  uint64_t j, step;
+  uint32_t q;
+  pair_slot(j, q, step);
+  const Fe* __restrict__ X = q ? M : A;
+  const Fe* __restrict__ Z = q ? P : S;
+  Fe* __restrict__ X2 = q ? M2 : A2;
+  Fe* __restrict__ Z2 = q ? P2 : S2;
+  for (; j < h; j += step) {
+    const Fe x0 = ld_fe(X, j), x1 = ld_fe(X, j + h), x2 = ld_fe(X, j + 2 * h), x3 = ld_fe(X, j + 3 * h);
+    const Fe z0 = ld_fe(Z, j), z1 = ld_fe(Z, j + h), z2 = ld_fe(Z, j + 2 * h), z3 = ld_fe(Z, j + 3 * h);
+#if ZK_ROUND_LOADS_FIRST
+    __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
+#endif
+    const Fe a0 = fold1<F>(x0, x2, r), a1 = fold1<F>(x1, x3, r);
+    const Fe s0 = fold1<F>(z0, z2, r), s1 = fold1<F>(z1, z3, r);
+    st_fe(X2, j, a0);
+    st_fe(X2, j + h, a1);
+    st_fe(Z2, j, s0);
+    st_fe(Z2, j + h, s1);
+    wide_mac<F>(w0, a0, s0);
+    wide_mac<F>(w2, at2<F>(a0, a1), at2<F>(s0, s1));
   }
-  block_reduce_store<F, 2>(acc, partials);
+  Fe acc[2] = {wide_redc<F>(w0), wide_redc<F>(w2)};
+  block_reduce_finish<F, 2>(acc, sink);
+}
+
+// ---------------------------------------------------------------------------
+// Same round as k_gkr_round for SMALL tables, where a thread-per-pair kernel is
+// latency-bound (one wave serialises 12 dependent 256-bit multiplies). Here 8
+// lanes share a pair: lane s folds table s>>1, half s&1 (one multiply); odd
+// lanes turn (lo, hi) into X(2) = 2 hi - lo; lanes {0,1,4,5} multiply with lane
+// s+2 (A*S / M*P at t = 0 and t = 2). Critical path: 2 multiplies.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ Fe shfl_fe(const Fe& x, int src) {
+  Fe r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = __shfl(x.v[i], src, 64);
+  return r;
+}
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                            const Fe* __restrict__ M, const Fe* __restrict__ P,
+                                                            Fe* __restrict__ A2, Fe* __restrict__ S2,
+                                                            Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h,
+                                                            Fe r, RoundSink sink) {
+  const uint32_t lane = threadIdx.x & 63, s = threadIdx.x & 7, tb = s >> 1, half = s & 1;
+  const Fe* __restrict__ X = tb == 0 ? A : tb == 1 ? S : tb == 2 ? M : P;
+  Fe* __restrict__ Y = tb == 0 ? A2 : tb == 1 ? S2 : tb == 2 ? M2 : P2;
+  Fe acc[2] = {fe_zero<F>(), fe_zero<F>()};
+  const uint64_t stride = (uint64_t)gridDim.x * (kBlock / 8);
+  // the loop bound is uniform per 8-lane group (and per wave: 8 groups share j's stride)
+  for (uint64_t j = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 3; j < h; j += stride) {
+    const uint64_t o = j + half * h;
+    const Fe f = fold1<F>(ld_fe(X, o), ld_fe(X, o + 2 * h), r);
+    st_fe(Y, o, f);
+    const Fe lo = shfl_fe(f, (int)(lane & ~1u));        // the group's lo for this table
+    const Fe v = half ? at2<F>(lo, f) : f;               // even: X(0), odd: X(2)
+    const Fe partner = shfl_fe(v, (int)((lane + 2) & 63));
+    const Fe prod = fe_mul<F>(v, partner);
+    if (s == 0 || s == 4) acc[0] = fe_add<F>(acc[0], prod);
+    if (s == 1 || s == 5) acc[1] = fe_add<F>(acc[1], prod);
+  }
+  block_reduce_finish<F, 2>(acc, sink);
 }
 
 // ---------------------------------------------------------------------------
@@ -155,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round(const Fe* __restrict__ A, 
 // ---------------------------------------------------------------------------
 template <class F, bool FIRST>
 __global__ __launch_bounds__(kBlock) void k_sc_round(const Fe* __restrict__ X, Fe* __restrict__ Y, uint64_t h, Fe r,
-                                                     Fe* __restrict__ partials) {
+                                                     RoundSink sink) {
   Fe acc[2] = {fe_zero<F>(), fe_zero<F>()};
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < h; j += stride) {
@@ -171,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_sc_round(const Fe* __restrict__ X, F
       acc[1] = fe_add<F>(acc[1], f1);
     }
   }
-  block_reduce_store<F, 2>(acc, partials);
+  block_reduce_finish<F, 2>(acc, sink);
 }
 
 // ---------------------------------------------------------------------------
@@ -204,47 +398,6 @@ __global__ __launch_bounds__(kBlock) void k_fold4(const Fe* __restrict__ A, cons
     st_fe(S2, v, fold1<F>(ld_fe(S, v), ld_fe(S, v + half), r));
     st_fe(M2, v, fold1<F>(ld_fe(M, v), ld_fe(M, v + half), r));
     st_fe(P2, v, fold1<F>(ld_fe(P, v), ld_fe(P, v + half), r));
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Block partials [nblk][K] -> K sums, written limb-split: out[k*8+i] = limb i
-// (32 bits in a u64 lane). The split form is what the multi-GPU all-reduce
-// sums exactly (ncclUint64); the host folds it back mod p.
-// ---------------------------------------------------------------------------
-template <class F, int K>
-__global__ __launch_bounds__(kBlock) void k_reduce_partials(const Fe* __restrict__ partials, uint32_t nblk,
-                                                            uint64_t* __restrict__ out) {
-  Fe acc[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) acc[k] = fe_zero<F>();
-  for (uint32_t b = threadIdx.x; b < nblk; b += kBlock) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = fe_add<F>(acc[k], ld_fe(partials, (uint64_t)b * K + k));
-  }
-  __shared__ Fe sm[kBlock / 64][K];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      Fe o;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o.v[i] = __shfl_xor(acc[k].v[i], off, 64);
-      acc[k] = fe_add<F>(acc[k], o);
-    }
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) sm[wave][k] = acc[k];
-  }
-  __syncthreads();
-  if (threadIdx.x < K) {
-    Fe s = sm[0][threadIdx.x];
-#pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) s = fe_add<F>(s, sm[w][threadIdx.x]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) out[threadIdx.x * 8 + i] = s.v[i];
   }
 }
 

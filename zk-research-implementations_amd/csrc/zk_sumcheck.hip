@@ -10,10 +10,13 @@
 // The host side holds only O(1)-per-round scalar work and the transcript;
 // every table-sized operation runs on the GPU.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -181,8 +184,10 @@ struct zk_ctx {
   DevBuf input;    // host-API staging (4 tables)
   DevBuf partials;
   DevBuf small;    // reduce output (u64[32]) + flag + gather buffers
-  uint64_t* h_red = nullptr;  // pinned readback
-  bool timing = false;
+  uint64_t* h_red = nullptr;  // pinned, device-mapped: round sums (u64[32]) + flag word at [64]
+  uint32_t tag = 0;           // last round tag handed to a kernel
+  uint64_t lanes_max_pairs = 1u << 15;  // rounds with <= this many pairs use 8 lanes per pair
+  uint32_t timing = 0;  // bit k: time launches of kernel kind k
   zk_stats stats{};
   struct Pending {
     int kind;
@@ -194,32 +199,52 @@ struct zk_ctx {
   int rank = 0, world = 1;
   CommKind comm = COMM_NONE;
   zk_allreduce_u64_fn ar = nullptr;
-  zk_allgather_fn ag = nullptr;
+  bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   void* user = nullptr;
   ncclComm_t nccl = nullptr;
 };
 
 namespace {
-constexpr size_t kSmallBytes = 64 * 1024;
+// small device area: [0,1024) round sums / flags / counter, [1024, +64 KiB)
+// all-reduce bounce buffer (<= 256 ranks x 256 B), then the tail's 4 local
+// elements and the gathered 4 x world tables
+constexpr size_t kSmallBytes = 160 * 1024;
 uint64_t* d_red(zk_ctx* c) { return reinterpret_cast<uint64_t*>(c->small.p); }
 uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 512); }
+uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 768); }
+uint32_t* h_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(c->h_red + 64); }
 char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 1024; }
 
 void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
 
-uint32_t grid_for(zk_ctx* c, uint64_t work) {
-  const uint64_t cap = (uint64_t)c->num_cus * 8;
+// At most one resident wave of 256-thread blocks (blocks/CU from the
+// kernel's register budget), grid-striding over the rest: no tail of
+// half-empty CUs.
+template <class K>
+uint32_t grid_for(zk_ctx* c, uint64_t work, K kernel) {
+  static thread_local std::vector<std::pair<const void*, int>> cache;
+  int per_cu = 0;
+  for (auto& e : cache)
+    if (e.first == reinterpret_cast<const void*>(kernel)) per_cu = e.second;
+  if (per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, zk::kBlock, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    cache.push_back({reinterpret_cast<const void*>(kernel), per_cu});
+  }
+  const uint64_t cap = (uint64_t)c->num_cus * per_cu;
   uint64_t g = (work + zk::kBlock - 1) / zk::kBlock;
   if (g < 1) g = 1;
   return (uint32_t)std::min<uint64_t>(g, cap);
 }
 
 // Launch wrapper: counts algorithmic bytes / multiplications per kernel kind
-// and, when timing is on, brackets the launch with HIP events on c->stream.
-template <class L>
-void launch(zk_ctx* c, int kind, double bytes, double muls, L&& body) {
+// and, when timing is on, has the dispatch packet itself record start/stop
+// events on c->stream (hipExtLaunchKernelGGL: no extra API calls per launch).
+template <class Kern, class... Args>
+void launch(zk_ctx* c, int kind, double bytes, double muls, Kern kernel, uint32_t grid, Args... args) {
   zk_ctx::Pending p{kind, nullptr, nullptr};
-  if (c->timing) {
+  const bool timed = (c->timing >> kind) & 1u;
+  if (timed) {
     if (c->ev_free.empty()) {
       hipEvent_t a, b;
       HIPCK(hipEventCreate(&a));
@@ -229,14 +254,10 @@ void launch(zk_ctx* c, int kind, double bytes, double muls, L&& body) {
     p.a = c->ev_free.back().first;
     p.b = c->ev_free.back().second;
     c->ev_free.pop_back();
-    HIPCK(hipEventRecord(p.a, c->stream));
   }
-  body();
+  hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(zk::kBlock), 0, c->stream, p.a, p.b, 0, args...);
   HIPCK(hipGetLastError());
-  if (c->timing) {
-    HIPCK(hipEventRecord(p.b, c->stream));
-    c->pending.push_back(p);
-  }
+  if (timed) c->pending.push_back(p);
   c->stats.launches[kind] += 1;
   c->stats.alg_bytes[kind] += bytes;
   c->stats.field_muls[kind] += muls;
@@ -281,28 +302,78 @@ Fe from_limb_sums(const uint64_t* w) {
 }
 
 // ---------------------------------------------------------------------------
-// partial sums: block partials (already written by the round kernel) ->
-// K limb-split sums -> [all-reduce over ranks] -> host field elements
+// Round sums: the round kernel's last block writes the K sums (limb-split)
+// straight into pinned host memory and raises a flag; the host spins on the
+// flag (no stream synchronisation, no copy kernel). Across ranks over RCCL the
+// sums go to device memory, are all-reduced on the stream, then published.
 // ---------------------------------------------------------------------------
+bool multi_rank(zk_ctx* c) { return (c->world > 1 || c->force_coll) && c->comm != COMM_NONE; }
+
+// In-place SUM of n u64 over all ranks (host memory in/out). RCCL runs on the
+// ctx stream through a device bounce buffer; a host communicator runs its callback.
+void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
+  if (c->comm == COMM_RCCL) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(d_gather(c));
+    HIPCK(hipMemcpyAsync(d, w, n * 8, hipMemcpyHostToDevice, c->stream));
+    NCCLCK(ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, c->stream));
+    HIPCK(hipMemcpyAsync(w, d, n * 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+  } else if (c->comm == COMM_HOST) {
+    if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+  } else {
+    fail(ZK_ECOMM, "no communicator attached");
+  }
+  c->stats.collectives += 1;
+}
+
+zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
+  zk::RoundSink s;
+  s.partials = c->partials.fe();
+  s.counter = d_counter(c);
+  s.tag = ++c->tag;
+  const bool via_rccl = across_ranks && multi_rank(c) && c->comm == COMM_RCCL;
+  s.dev_out = via_rccl ? d_red(c) : nullptr;
+  s.host_out = via_rccl ? nullptr : c->h_red;
+  s.host_flag = via_rccl ? nullptr : h_flag(c);
+  return s;
+}
+
+void wait_flag(zk_ctx* c, uint32_t tag) {
+  const uint32_t* f = h_flag(c);
+  uint64_t spins = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(f, __ATOMIC_ACQUIRE) != tag) {
+    __builtin_ia32_pause();
+    if ((++spins & 0xFFFF) == 0) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) fail(ZK_EDEVICE, std::string("round kernel failed: ") + hipGetErrorString(e));
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if ((e == hipSuccess && s > 1.0) || s > 60.0) fail(ZK_EDEVICE, "round result flag never arrived");
+    }
+  }
+  c->stats.host_syncs += 1;
+}
+
 template <class F, int K>
-void read_sums(zk_ctx* c, uint32_t nblk, bool across_ranks, Fe (&out)[K]) {
-  launch(c, ZK_K_REDUCE, (double)nblk * K * 32, 0,
-         [&] { zk::k_reduce_partials<F, K><<<1, zk::kBlock, 0, c->stream>>>(c->partials.fe(), nblk, d_red(c)); });
-  const bool multi = across_ranks && c->world > 1;
+void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, Fe (&out)[K]) {
+  const bool multi = across_ranks && multi_rank(c);
   if (multi && c->comm == COMM_RCCL) {
     NCCLCK(ncclAllReduce(d_red(c), d_red(c), K * 8, ncclUint64, ncclSum, c->nccl, c->stream));
     c->stats.collectives += 1;
+    zk::k_publish<<<1, 64, 0, c->stream>>>(d_red(c), K * 8, c->h_red, h_flag(c), sk.tag);
+    HIPCK(hipGetLastError());
   }
-  HIPCK(hipMemcpyAsync(c->h_red, d_red(c), K * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-  sync(c);
+  wait_flag(c, sk.tag);
+  uint64_t w[K * 8];
+  for (int i = 0; i < K * 8; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
   if (multi && c->comm == COMM_HOST) {
-    if (c->ar(c->user, c->h_red, K * 8) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+    if (c->ar(c->user, w, K * 8) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
     c->stats.collectives += 1;
   }
-  for (int k = 0; k < K; ++k) out[k] = from_limb_sums<F>(c->h_red + 8 * k);
+  for (int k = 0; k < K; ++k) out[k] = from_limb_sums<F>(w + 8 * k);
 }
 
-void ensure_partials(zk_ctx* c) { c->partials.ensure((size_t)c->num_cus * 8 * 3 * 32); }
+void ensure_partials(zk_ctx* c) { c->partials.ensure((size_t)c->num_cus * 8 * 4 * 32); }
 
 // ---------------------------------------------------------------------------
 // GKR sum-check rounds
@@ -347,30 +418,33 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint32_t k = k0 + i;
     const uint64_t size = L >> i;  // table length in this round
     const uint64_t h = size / 2;   // pairs
-    const uint32_t grid = grid_for(c, h);
     Fe e0, e1, e2;
     if (i == 0) {
-      launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, [&] {
-        zk::k_gkr_round0<F><<<grid, zk::kBlock, 0, c->stream>>>(cur[0], cur[1], cur[2], cur[3], h, c->partials.fe());
-      });
+      const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round0<F>);
+      const zk::RoundSink sk = make_sink(c, across_ranks);
+      launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, zk::k_gkr_round0<F>, grid, cur[0], cur[1], cur[2], cur[3], h, sk);
       Fe s[3];
-      read_sums<F, 3>(c, grid, across_ranks, s);
+      collect_sums<F, 3>(c, sk, across_ranks, s);
       e0 = s[0];
       e1 = s[1];
       e2 = s[2];
     } else {
+      const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round<F>);
       // fold previous (size 2*size) -> work[(i+1)&1] (size `size`) and evaluate;
       // work[0] holds the size-L/2 level, work[1] the size-L/4 level, ...
       Fe* w = c->work[(i + 1) & 1].fe();
       Fe* nx[4] = {w, w + size, w + 2 * size, w + 3 * size};
       const Fe rr = r;
-      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, [&] {
-        zk::k_gkr_round<F><<<grid, zk::kBlock, 0, c->stream>>>(cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2],
-                                                               nx[3], h, rr, c->partials.fe());
-      });
+      const zk::RoundSink sk = make_sink(c, across_ranks);
+      if (h <= c->lanes_max_pairs) {  // latency-bound size: 8 lanes per pair
+        const uint32_t g8 = grid_for(c, 8 * h, zk::k_gkr_round_lanes<F>);
+        launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round_lanes<F>, g8, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rr, sk);
+      } else {
+        launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rr, sk);
+      }
       for (int t = 0; t < 4; ++t) cur[t] = nx[t];
       Fe s[2];
-      read_sums<F, 2>(c, grid, across_ranks, s);
+      collect_sums<F, 2>(c, sk, across_ranks, s);
       e0 = s[0];
       e2 = s[1];
       // s_{k-1}(X) = sum_j f(X, j) is exact (degree 2 in X), so
@@ -399,44 +473,38 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   const Fe* cur[4] = {dT[0], dT[1], dT[2], dT[3]};
   Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
   gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r);
-  if (lg == 0) return;
+  if (lg == 0) {
+    sync(c);  // settles event timings; the results are already on the host
+    return;
+  }
 
   // ---- multi-GPU tail: every rank now holds 1 (folded) element per table ----
-  Fe* send = reinterpret_cast<Fe*>(d_gather(c));  // 4 elements
+  // Gather the G x 4 elements with the same exact all-reduce as the rounds:
+  // each rank fills only its own slot of a zeroed limb-split vector.
+  Fe* send = reinterpret_cast<Fe*>(d_gather(c) + 65536);  // 4 elements, after the bounce buffer
   if (nloc > 0) {
     Fe* s4[4] = {send, send + 1, send + 2, send + 3};
-    const Fe rr = r;
-    launch(c, ZK_K_FOLD, 4 * 96.0, 4.0, [&] {
-      zk::k_fold4<F><<<1, zk::kBlock, 0, c->stream>>>(cur[0], cur[1], cur[2], cur[3], s4[0], s4[1], s4[2], s4[3],
-                                                      1, rr);
-    });
+    launch(c, ZK_K_FOLD, 4 * 96.0, 4.0, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], s4[0], s4[1], s4[2],
+           s4[3], (uint64_t)1, r);
   } else {
-    for (int t = 0; t < 4; ++t)
-      HIPCK(hipMemcpyAsync(send + t, cur[t], 32, hipMemcpyDeviceToDevice, c->stream));
+    for (int t = 0; t < 4; ++t) HIPCK(hipMemcpyAsync(send + t, cur[t], 32, hipMemcpyDeviceToDevice, c->stream));
   }
-  std::vector<Fe> gathered((size_t)G * 4);
-  if (c->comm == COMM_RCCL) {
-    Fe* recv = send + 4;
-    NCCLCK(ncclAllGather(send, recv, 4 * 32, ncclUint8, c->nccl, c->stream));
-    c->stats.collectives += 1;
-    HIPCK(hipMemcpyAsync(gathered.data(), recv, (size_t)G * 128, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-  } else {
-    Fe mine[4];
-    HIPCK(hipMemcpyAsync(mine, send, 128, hipMemcpyDeviceToHost, c->stream));
-    sync(c);
-    if (c->comm != COMM_HOST || c->ag(c->user, mine, gathered.data(), 128) != 0)
-      fail(ZK_ECOMM, "all-gather failed");
-    c->stats.collectives += 1;
-  }
+  Fe mine[4];
+  HIPCK(hipMemcpyAsync(mine, send, 128, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  std::vector<uint64_t> w((size_t)G * 4 * 8, 0);
+  for (int t = 0; t < 4; ++t)
+    for (int i = 0; i < 8; ++i) w[((size_t)c->rank * 4 + t) * 8 + i] = mine[t].v[i];
+  allreduce_host(c, w.data(), w.size());
   // global table t, index g = rank g's element (local index 0 <-> global g)
   std::vector<Fe> tabs((size_t)4 * G);
   for (int g = 0; g < G; ++g)
-    for (int t = 0; t < 4; ++t) tabs[(size_t)t * G + g] = gathered[(size_t)g * 4 + t];
-  Fe* stage = send + 4 + 4 * G;  // after the send/recv records in the gather area
+    for (int t = 0; t < 4; ++t) tabs[(size_t)t * G + g] = from_limb_sums<F>(&w[((size_t)g * 4 + t) * 8]);
+  Fe* stage = send + 4;
   HIPCK(hipMemcpyAsync(stage, tabs.data(), tabs.size() * 32, hipMemcpyHostToDevice, c->stream));
   const Fe* tcur[4] = {stage, stage + G, stage + 2 * G, stage + 3 * G};
   gkr_phase<F>(c, tcur, lg, nloc, false, tr, out, claim, r);
+  sync(c);
 }
 
 // ---------------------------------------------------------------------------
@@ -460,13 +528,12 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
   c->work[0].ensure(std::max<uint64_t>(N / 2, 1) * 32);
   c->work[1].ensure(std::max<uint64_t>(N / 4, 1) * 32);
   uint64_t h = N / 2;
-  uint32_t grid = grid_for(c, h);
-  launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, [&] {
-    zk::k_sc_round<F, true><<<grid, zk::kBlock, 0, c->stream>>>(dX, nullptr, h, zk::fe_zero<F>(), c->partials.fe());
-  });
-  tr->h.update(table_bytes, nbytes);
+  uint32_t grid = grid_for(c, h, zk::k_sc_round<F, true>);
+  zk::RoundSink sk = make_sink(c, false);
+  launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, zk::k_sc_round<F, true>, grid, dX, nullptr, h, zk::fe_zero<F>(), sk);
+  tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps the GPU
   Fe s[2];
-  read_sums<F, 2>(c, grid, false, s);
+  collect_sums<F, 2>(c, sk, false, s);
   claimed = zk::fe_add<F>(s[0], s[1]);  // = sum of the table (:29)
   absorb<F>(tr, &claimed, 1);
   const Fe* cur = dX;
@@ -474,20 +541,20 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
   for (uint32_t k = 0; k < n; ++k) {
     if (k > 0) {
       h = (N >> k) / 2;
-      grid = grid_for(c, h);
+      grid = grid_for(c, h, zk::k_sc_round<F, false>);
       Fe* nx = c->work[(k + 1) & 1].fe();
       const Fe rr = r;
-      launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, [&] {
-        zk::k_sc_round<F, false><<<grid, zk::kBlock, 0, c->stream>>>(cur, nx, h, rr, c->partials.fe());
-      });
+      sk = make_sink(c, false);
+      launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, zk::k_sc_round<F, false>, grid, cur, nx, h, rr, sk);
       cur = nx;
-      read_sums<F, 2>(c, grid, false, s);
+      collect_sums<F, 2>(c, sk, false, s);
     }
     rp[2 * k] = s[0];
     rp[2 * k + 1] = s[1];
     absorb<F>(tr, s, 2);
     r = challenge<F>(tr);
   }
+  sync(c);
 }
 
 // MultilinearPoly::evaluate on device: n folds at bit 0, ping-pong workspaces
@@ -506,12 +573,10 @@ Fe mle_evaluate_device(zk_ctx* c, const Fe* dX, uint32_t n, const std::vector<Fe
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t half = N >> (i + 1);
     Fe* nx = c->work[i & 1].fe();
-    const uint32_t grid = grid_for(c, half);
+    const uint32_t grid = grid_for(c, half, zk::k_fold<F>);
     const Fe r = pt[i];
     const uint32_t s = n - 1 - i;  // bit 0 of the current (n-i)-variable table
-    launch(c, ZK_K_FOLD, 96.0 * half, (double)half, [&] {
-      zk::k_fold<F><<<grid, zk::kBlock, 0, c->stream>>>(cur, nx, half, s, r);
-    });
+    launch(c, ZK_K_FOLD, 96.0 * half, (double)half, zk::k_fold<F>, grid, cur, nx, half, s, r);
     cur = nx;
   }
   HIPCK(hipMemcpyAsync(&res, cur, 32, hipMemcpyDeviceToHost, c->stream));
@@ -527,12 +592,10 @@ void upload(zk_ctx* c, zk_repr repr, const zk_fe* host, size_t n, Fe* dev) {
   if (n == 0) return;
   HIPCK(hipMemcpyAsync(dev, host, n * 32, hipMemcpyHostToDevice, c->stream));
   HIPCK(hipMemsetAsync(d_flag(c), 0, 4, c->stream));
-  const uint32_t grid = grid_for(c, n);
-  launch(c, ZK_K_CONVERT, 32.0 * n, 0,
-         [&] { zk::k_check_canonical<F><<<grid, zk::kBlock, 0, c->stream>>>(dev, n, d_flag(c)); });
+  const uint32_t grid = grid_for(c, n, zk::k_check_canonical<F>);
+  launch(c, ZK_K_CONVERT, 32.0 * n, 0, zk::k_check_canonical<F>, grid, dev, n, d_flag(c));
   if (repr == ZK_REPR_CANONICAL)
-    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n,
-           [&] { zk::k_convert<F, true><<<grid, zk::kBlock, 0, c->stream>>>(dev, dev, n); });
+    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n, zk::k_convert<F, true>, grid, dev, dev, n);
   uint32_t bad = 0;
   HIPCK(hipMemcpyAsync(&bad, d_flag(c), 4, hipMemcpyDeviceToHost, c->stream));
   sync(c);
@@ -544,9 +607,8 @@ void download(zk_ctx* c, zk_repr repr, const Fe* dev, size_t n, zk_fe* host) {
   if (repr == ZK_REPR_CANONICAL) {
     c->work[1].ensure(std::max(c->work[1].bytes, n * 32));
     Fe* tmp = c->work[1].fe();
-    const uint32_t grid = grid_for(c, n);
-    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n,
-           [&] { zk::k_convert<F, false><<<grid, zk::kBlock, 0, c->stream>>>(dev, tmp, n); });
+    const uint32_t grid = grid_for(c, n, zk::k_convert<F, false>);
+    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n, zk::k_convert<F, false>, grid, dev, tmp, n);
     dev = tmp;
   }
   HIPCK(hipMemcpyAsync(host, dev, n * 32, hipMemcpyDeviceToHost, c->stream));
@@ -598,12 +660,16 @@ int zk_ctx_create(int device, zk_ctx** out) {
       fail(ZK_EDEVICE, std::string("kernels are built for gfx950, device is ") + prop.gcnArchName);
     auto* c = new zk_ctx();
     c->device = device;
+    if (const char* e = getenv("ZK_LANES_MAX_PAIRS")) c->lanes_max_pairs = strtoull(e, nullptr, 0);  // tuning knob
+    if (const char* e = getenv("ZK_FORCE_COLLECTIVES")) c->force_coll = atoi(e) != 0;
     c->num_cus = prop.multiProcessorCount;
     try {
       bind(c);
       HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       c->small.ensure(kSmallBytes);
-      HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), 4096, hipHostMallocDefault));
+      HIPCK(hipMemset(c->small.p, 0, kSmallBytes));
+      HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), 4096, hipHostMallocMapped | hipHostMallocCoherent));
+      memset(c->h_red, 0, 4096);
     } catch (...) {
       zk_ctx_destroy(c);
       throw;
@@ -635,7 +701,13 @@ void zk_ctx_destroy(zk_ctx* c) {
 int zk_ctx_set_timing(zk_ctx* c, int enable) {
   return guarded([&] {
     require(c, "ctx is null");
-    c->timing = enable != 0;
+    c->timing = enable ? (1u << ZK_K_KINDS) - 1 : 0u;
+  });
+}
+int zk_ctx_set_timing_mask(zk_ctx* c, uint32_t kind_mask) {
+  return guarded([&] {
+    require(c, "ctx is null");
+    c->timing = kind_mask & ((1u << ZK_K_KINDS) - 1);
   });
 }
 int zk_ctx_get_stats(const zk_ctx* c, zk_stats* out) {
@@ -698,11 +770,9 @@ int zk_mle_partial_evaluate(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe
       c->input.ensure(N * 32);
       upload<F>(c, repr, evals, N, c->input.fe());
       c->work[0].ensure(half * 32);
-      const uint32_t grid = grid_for(c, half);
+      const uint32_t grid = grid_for(c, half, zk::k_fold<F>);
       const uint32_t s = nvars - 1 - bit;
-      launch(c, ZK_K_FOLD, 96.0 * half, (double)half, [&] {
-        zk::k_fold<F><<<grid, zk::kBlock, 0, c->stream>>>(c->input.fe(), c->work[0].fe(), half, s, r);
-      });
+      launch(c, ZK_K_FOLD, 96.0 * half, (double)half, zk::k_fold<F>, grid, c->input.fe(), c->work[0].fe(), half, s, r);
       download<F>(c, repr, c->work[0].fe(), half, out);
     });
   });
@@ -922,10 +992,8 @@ int zk_dev_synth_fill(zk_ctx* c, zk_field field, void* dev, uint64_t count, uint
     dispatch(field, [&](auto f) {
       using F = decltype(f);
       const uint64_t key = zk::splitmix64(zk::splitmix64(seed) + table);
-      const uint32_t grid = grid_for(c, count);
-      launch(c, ZK_K_SYNTH, 32.0 * count, (double)count, [&] {
-        zk::k_synth<F><<<grid, zk::kBlock, 0, c->stream>>>(reinterpret_cast<Fe*>(dev), count, key, index0, stride);
-      });
+      const uint32_t grid = grid_for(c, count, zk::k_synth<F>);
+      launch(c, ZK_K_SYNTH, 32.0 * count, (double)count, zk::k_synth<F>, grid, reinterpret_cast<Fe*>(dev), count, key, index0, stride);
       sync(c);
     });
   });
@@ -941,12 +1009,9 @@ int zk_dev_mle_partial_evaluate(zk_ctx* c, zk_field field, const void* d_in, uin
       using F = decltype(f);
       const Fe r = in_mont<F>(repr, *value);
       const uint64_t half = (uint64_t)1 << (nvars - 1);
-      const uint32_t grid = grid_for(c, half);
+      const uint32_t grid = grid_for(c, half, zk::k_fold<F>);
       const uint32_t s = nvars - 1 - bit;
-      launch(c, ZK_K_FOLD, 96.0 * half, (double)half, [&] {
-        zk::k_fold<F><<<grid, zk::kBlock, 0, c->stream>>>(reinterpret_cast<const Fe*>(d_in),
-                                                          reinterpret_cast<Fe*>(d_out), half, s, r);
-      });
+      launch(c, ZK_K_FOLD, 96.0 * half, (double)half, zk::k_fold<F>, grid, reinterpret_cast<const Fe*>(d_in), reinterpret_cast<Fe*>(d_out), half, s, r);
       sync(c);
     });
   });
@@ -973,10 +1038,9 @@ int zk_dev_gkr_sumcheck_prove(zk_ctx* c, zk_field field, const void* const d_tab
 }
 
 // ---- multi-GPU ----
-int zk_ctx_attach_host_comm(zk_ctx* c, int rank, int world, zk_allreduce_u64_fn allreduce, zk_allgather_fn allgather,
-                            void* user) {
+int zk_ctx_attach_host_comm(zk_ctx* c, int rank, int world, zk_allreduce_u64_fn allreduce, void* user) {
   return guarded([&] {
-    require(c && allreduce && allgather, "null argument");
+    require(c && allreduce, "null argument");
     require(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
     require(rank >= 0 && rank < world, "rank out of range");
     if (c->nccl) {
@@ -987,7 +1051,6 @@ int zk_ctx_attach_host_comm(zk_ctx* c, int rank, int world, zk_allreduce_u64_fn 
     c->world = world;
     c->comm = COMM_HOST;
     c->ar = allreduce;
-    c->ag = allgather;
     c->user = user;
   });
 }
@@ -1038,7 +1101,7 @@ int zk_dev_gkr_sumcheck_prove_sharded(zk_ctx* c, zk_field field, const void* con
     for (int t = 0; t < 4; ++t) require(d_local_tables[t] != nullptr, "null table");
     require(pow2_ok(nvars_local), "table too large");
     require(c->world == 1 || c->comm != COMM_NONE, "no communicator attached");
-    require(1024 + 128 + (size_t)c->world * 256 <= kSmallBytes, "world too large for the gather buffer");
+    require(c->world <= 256, "world too large for the gather buffers");
     bind(c);
     dispatch(field, [&](auto f) {
       using F = decltype(f);

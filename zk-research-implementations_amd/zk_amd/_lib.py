@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libzksumcheck.so")
+LIB_PATH = os.environ.get("ZK_LIB_PATH") or os.path.join(_HERE, "_lib", "libzksumcheck.so")  # override: A/B builds
 PKG_ROOT = os.path.dirname(_HERE)
 
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
@@ -37,7 +37,6 @@ class ZkStats(C.Structure):
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t)
-ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 # name -> (restype, argtypes); every symbol declared in include/zk_sumcheck.h
 P, I, U32, U64, SZ = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64, C.c_size_t
@@ -47,6 +46,7 @@ SIGNATURES = {
     "zk_ctx_create": (I, [I, C.POINTER(C.c_void_p)]),
     "zk_ctx_destroy": (None, [P]),
     "zk_ctx_set_timing": (I, [P, I]),
+    "zk_ctx_set_timing_mask": (I, [P, U32]),
     "zk_ctx_get_stats": (I, [P, C.POINTER(ZkStats)]),
     "zk_ctx_reset_stats": (I, [P]),
     "zk_transcript_new": (P, []),
@@ -68,7 +68,7 @@ SIGNATURES = {
     "zk_dev_synth_fill": (I, [P, I, P, U64, U64, U32, U64, U64]),
     "zk_dev_mle_partial_evaluate": (I, [P, I, P, U32, U32, I, P, P]),
     "zk_dev_gkr_sumcheck_prove": (I, [P, I, P, U32, I, P, P, P, P, P]),
-    "zk_ctx_attach_host_comm": (I, [P, I, I, ALLREDUCE_FN, ALLGATHER_FN, P]),
+    "zk_ctx_attach_host_comm": (I, [P, I, I, ALLREDUCE_FN, P]),
     "zk_comm_get_unique_id": (I, [P]),
     "zk_ctx_attach_rccl": (I, [P, I, I, P]),
     "zk_ctx_detach_comm": (I, [P]),

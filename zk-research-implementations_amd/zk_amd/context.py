@@ -37,6 +37,13 @@ class Context:
     def set_timing(self, enable: bool) -> None:
         check(lib().zk_ctx_set_timing(self.h, int(bool(enable))))
 
+    def set_timing_kinds(self, kinds) -> None:
+        """Time only launches of these kernel kinds (names from KERNEL_KINDS)."""
+        mask = 0
+        for k in kinds:
+            mask |= 1 << KERNEL_KINDS.index(k)
+        check(lib().zk_ctx_set_timing_mask(self.h, mask))
+
     def reset_stats(self) -> None:
         check(lib().zk_ctx_reset_stats(self.h))
 
@@ -77,30 +84,19 @@ class Context:
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
         check(lib().zk_ctx_attach_rccl(self.h, rank, world, buf))
 
-    def attach_host_comm(self, rank: int, world: int, allreduce, allgather) -> None:
-        """allreduce(np.ndarray[uint64]) -> None (in-place SUM);
-        allgather(bytes) -> bytes (rank-ordered concatenation)."""
+    def attach_host_comm(self, rank: int, world: int, allreduce) -> None:
+        """allreduce(np.ndarray[uint64]) -> None: in-place SUM over all ranks."""
 
         def _ar(user, data, count):
             try:
-                arr = np.ctypeslib.as_array(data, shape=(count,))
-                allreduce(arr)
+                allreduce(np.ctypeslib.as_array(data, shape=(count,)))
                 return 0
             except Exception:  # the C side turns this into ZK_ECOMM
                 return 1
 
-        def _ag(user, send, recv, nbytes):
-            try:
-                mine = C.string_at(send, nbytes)
-                allb = allgather(mine)
-                C.memmove(recv, allb, len(allb))
-                return 0
-            except Exception:
-                return 1
-
-        cbs = (_lib.ALLREDUCE_FN(_ar), _lib.ALLGATHER_FN(_ag))
-        check(lib().zk_ctx_attach_host_comm(self.h, rank, world, cbs[0], cbs[1], None))
-        self._callbacks = cbs
+        cb = _lib.ALLREDUCE_FN(_ar)
+        check(lib().zk_ctx_attach_host_comm(self.h, rank, world, cb, None))
+        self._callbacks = cb
 
     def detach_comm(self) -> None:
         check(lib().zk_ctx_detach_comm(self.h))
