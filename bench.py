@@ -192,6 +192,12 @@ def main() -> None:
     kernel_ms = sum(v["ms"] for v in k.values()) / args.steps
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
 
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "r1_traffic.json")
+    if os.path.exists(tpath) and n == 24:
+        t = json.load(open(tpath))
+        traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
+        traffic_src = f"profiles/r1_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
     if rank == 0:
         out = {
             "metric": "GKR sum-check field-ops/sec + prover ms, 24-var BN254, 1/2/4/8 GPU",
@@ -222,10 +228,12 @@ def main() -> None:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "launches": rnd["launches"],
                 "avg_launch_us": rnd["ms"] * 1e3 / max(1, rnd["launches"]),
                 "alg_bytes_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]),
+                "alg_GB_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]) / 1e9,
             },
             "breakdown_per_step": {
                 "wall_ms": ms_per_step,

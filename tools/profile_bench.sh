@@ -1,0 +1,14 @@
+#!/bin/bash
+# Profile the default bench workload on the GPU box and keep the summaries.
+#   1) rocprofv3 --kernel-trace --stats           -> per-kernel durations
+#   2) rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE    -> HBM traffic (separate passes,
+#      gfx950: FETCH_SIZE counts half of a wide streaming read; corrected in
+#      tools/pmc_traffic.py)
+# usage: tools/profile_bench.sh <tag>   (outputs in gpurun_out/prof_<tag>*)
+set -e
+TAG=${1:-r1}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fold"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- $B > gpurun_out/prof_${TAG}_bench.json 2> gpurun_out/prof_${TAG}.err
+timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_${TAG}_fetch -o run -- $B > /dev/null 2>> gpurun_out/prof_${TAG}.err
+timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_${TAG}_write -o run -- $B > /dev/null 2>> gpurun_out/prof_${TAG}.err
