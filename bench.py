@@ -240,6 +240,8 @@ def main() -> None:
                 "timed_kernel_ms": kernel_ms,
                 "kernel_ms_by_kind": {kk: v["ms"] / args.steps for kk, v in k.items() if v["ms"]},
                 "host_syncs": st["host_syncs"] / args.steps,
+                "host_wait_ms": st["host_wait_us"] / 1e3 / args.steps,
+                "host_work_ms": st["host_work_us"] / 1e3 / args.steps,
                 "collectives": st["collectives"] / args.steps,
                 "field_muls": muls,
                 "launches_by_kind": {kk: v["launches"] / args.steps for kk, v in k.items() if v["launches"]},

@@ -83,7 +83,9 @@ typedef struct {
   double alg_bytes[ZK_K_KINDS];  /* algorithmic HBM bytes */
   double field_muls[ZK_K_KINDS]; /* Montgomery multiplications issued */
   uint64_t host_syncs;           /* device->host round trips */
-  uint64_t collectives;          /* all-reduce / all-gather calls */
+  uint64_t collectives;          /* all-reduce calls */
+  double host_wait_us;           /* host time spent waiting for round results */
+  double host_work_us;           /* host time from a round result to the next launch issued */
 } zk_stats;
 int zk_ctx_set_timing(zk_ctx* ctx, int enable);                /* all kinds on / off */
 int zk_ctx_set_timing_mask(zk_ctx* ctx, uint32_t kind_mask);   /* bit k = time ZK_K_k launches */

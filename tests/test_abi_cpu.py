@@ -145,3 +145,21 @@ def test_reference_shaped_constructors_panic_like_reference():
 def test_limbs_roundtrip():
     vals = [0, 1, (1 << 254) + 12345, (1 << 64) - 1]
     assert to_ints(as_limbs(vals)) == vals
+
+
+def test_single_hip_runtime_in_process():
+    """Loading the library and torch must leave exactly one libamdhip64 mapped
+    (two runtimes double-free at interpreter exit, see _lib.lib())."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from zk_amd import _lib; _lib.lib(); import torch\n"
+        "paths = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+        "print(len(paths), sorted(paths))\n"
+    ) % os.path.join(ROOT, "zk-research-implementations_amd")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.startswith("1 "), out.stdout
+    assert "free()" not in out.stderr and "double free" not in out.stderr, out.stderr[-2000:]

@@ -50,8 +50,9 @@ __device__ __forceinline__ Fe at2(const Fe& lo, const Fe& hi) {
 // raises host_flag = tag with a system-scope release; the host spins on that
 // flag instead of synchronising the stream.
 struct RoundSink {
-  Fe* partials;         // [gridDim.x][4]: one 128-B slot per block
-  uint32_t* counter;    // zero at launch; the last block resets it
+  Fe* partials;         // [gridDim.x + 8][4]: one 128-B slot per block, then 8 shard slots
+  uint32_t* counter;    // 9 counters, 128 B apart: 8 XCD shards + top; zero at launch, reset by their last user
+  uint64_t* accum;      // K*8 u64 limb-split accumulator (small grids); zero at launch, reset by the last block
   uint64_t* dev_out;    // K*8 u64 in device memory, or null
   uint64_t* host_out;   // K*8 u64 in pinned host memory, or null
   uint32_t* host_flag;  // pinned host word, or null
@@ -157,34 +158,19 @@ __device__ __forceinline__ void publish_totals(const Fe& t, const RoundSink& sk)
   }
 }
 
+// sum slots [first, first + count*stride) of `slots` (sc1 loads), spread over the block
 template <class F, int K>
-__device__ __forceinline__ void block_reduce_finish(Fe (&acc)[K], const RoundSink& sk) {
-  __shared__ W9 sm[kBlock / 64][K];
-  __shared__ uint32_t am_last;
-  const Fe s = block_sum<F, K>(acc, sm);
-  if (gridDim.x == 1) {  // single block: its sum is the total
-    publish_totals<K>(s, sk);
-    return;
-  }
-  if (threadIdx.x < K) st_fe_sc1(sk.partials, (uint64_t)blockIdx.x * 4 + threadIdx.x, s);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains before the signal
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    am_last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!am_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+__device__ __forceinline__ Fe sum_slots(Fe* slots, uint32_t first, uint32_t stride, uint32_t count,
+                                        W9 (&sm)[kBlock / 64][K]) {
   W9 tot[K];
 #pragma unroll
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int i = 0; i < 9; ++i) tot[k].w[i] = 0;
-  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kBlock) {
+  for (uint32_t b = threadIdx.x; b < count; b += kBlock) {
     Fe x[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = ld_fe_sc1(sk.partials, (uint64_t)b * 4 + k);
+    for (int k = 0; k < K; ++k) x[k] = ld_fe_sc1(slots, (uint64_t)(first + b * stride) * 4 + k);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       W9 y;
@@ -198,8 +184,95 @@ __device__ __forceinline__ void block_reduce_finish(Fe (&acc)[K], const RoundSin
 #pragma unroll
   for (int k = 0; k < K; ++k) red[k] = w9_reduce<F>(tot[k]);
   __syncthreads();  // sm is reused
-  const Fe t = block_sum<F, K>(red, sm);
-  if (threadIdx.x == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  return block_sum<F, K>(red, sm);
+}
+
+constexpr uint32_t kAtomicFaninMax = 64;  // grids up to this size fan in through limb atomics
+
+// Cross-block fan-in in two levels so no counter sees more than ~gridDim/8
+// arrivals (one device-scope counter serialises ~12 ns per arrival:
+// MI355X_MICROARCH.md "fanin"): blocks of shard s = blockIdx % 8 (one XCD
+// under round-robin placement — speed only, never correctness) meet on
+// counter s; each shard's last block sums the shard and meets the other
+// shards' last blocks on the top counter; the very last one publishes.
+template <class F, int K>
+__device__ __forceinline__ void block_reduce_finish(Fe (&acc)[K], const RoundSink& sk) {
+  __shared__ W9 sm[kBlock / 64][K];
+  __shared__ uint32_t am_last;
+  const Fe s = block_sum<F, K>(acc, sm);
+  const uint32_t G = gridDim.x;
+  if (G == 1) {  // single block: its sum is the total
+    publish_totals<K>(s, sk);
+    return;
+  }
+  if (G <= kAtomicFaninMax) {
+    // Small grid: every block adds its K sums limb by limb (no-return u64
+    // atomics at the device-coherent level; G * 2^32 < 2^64 stays exact),
+    // drains, and counts in; the last block reads the totals with sc1 loads.
+    if (threadIdx.x < K) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        __hip_atomic_fetch_add(sk.accum + threadIdx.x * 8 + i, (uint64_t)s.v[i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      am_last = prev == G - 1;
+    }
+    __syncthreads();
+    if (!am_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    Fe t = fe_zero<F>();
+    if (threadIdx.x < K) {
+      uint64_t w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        w[i] = __hip_atomic_exchange(sk.accum + threadIdx.x * 8 + i, (uint64_t)0, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);  // read and re-arm for the next launch
+      W9 y;
+      uint64_t c = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint64_t v = w[i] + c;
+        y.w[i] = (uint32_t)v;
+        c = v >> 32;
+      }
+      y.w[8] = (uint32_t)c;
+      t = w9_reduce<F>(y);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish_totals<K>(t, sk);
+    return;
+  }
+  const uint32_t shard = blockIdx.x & 7u, nshards = G < 8 ? G : 8u;
+  const uint32_t in_shard = (G - shard + 7u) / 8u;
+  if (threadIdx.x < K) st_fe_sc1(sk.partials, (uint64_t)blockIdx.x * 4 + threadIdx.x, s);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains before the signal
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev =
+        __hip_atomic_fetch_add(sk.counter + 32 * shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    am_last = prev == in_shard - 1;
+  }
+  __syncthreads();
+  if (!am_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
+  const Fe ts = sum_slots<F, K>(sk.partials, shard, 8u, in_shard, sm);
+  if (threadIdx.x < K) st_fe_sc1(sk.partials, (uint64_t)(G + shard) * 4 + threadIdx.x, ts);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(sk.counter + 32 * shard, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    const uint32_t prev = __hip_atomic_fetch_add(sk.counter + 32 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    am_last = prev == nshards - 1;
+  }
+  __syncthreads();
+  if (!am_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const Fe t = sum_slots<F, K>(sk.partials, G, 1u, nshards, sm);
+  if (threadIdx.x == 0) __hip_atomic_store(sk.counter + 32 * 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   publish_totals<K>(t, sk);
 }
 

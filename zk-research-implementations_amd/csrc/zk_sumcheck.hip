@@ -187,6 +187,8 @@ struct zk_ctx {
   uint64_t* h_red = nullptr;  // pinned, device-mapped: round sums (u64[32]) + flag word at [64]
   uint32_t tag = 0;           // last round tag handed to a kernel
   uint64_t lanes_max_pairs = 1u << 15;  // rounds with <= this many pairs use 8 lanes per pair
+  std::chrono::steady_clock::time_point work_t0;  // when the last round result was seen
+  bool work_open = false;
   uint32_t timing = 0;  // bit k: time launches of kernel kind k
   zk_stats stats{};
   struct Pending {
@@ -205,15 +207,18 @@ struct zk_ctx {
 };
 
 namespace {
-// small device area: [0,1024) round sums / flags / counter, [1024, +64 KiB)
-// all-reduce bounce buffer (<= 256 ranks x 256 B), then the tail's 4 local
-// elements and the gathered 4 x world tables
+// small device area: [0,512) round sums, [512] input check flag, [1024,2304)
+// fan-in counters (9 x 128 B), [2560,2816) limb accumulator (<= 3 x 8 u64),
+// [4096, +64 KiB) all-reduce bounce buffer
+// (<= 256 ranks x 256 B), then the tail's 4 local elements and the gathered
+// 4 x world tables
 constexpr size_t kSmallBytes = 160 * 1024;
 uint64_t* d_red(zk_ctx* c) { return reinterpret_cast<uint64_t*>(c->small.p); }
 uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 512); }
-uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 768); }
+uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 1024); }
+uint64_t* d_accum(zk_ctx* c) { return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(c->small.p) + 2560); }
 uint32_t* h_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(c->h_red + 64); }
-char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 1024; }
+char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 4096; }
 
 void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
 
@@ -257,6 +262,11 @@ void launch(zk_ctx* c, int kind, double bytes, double muls, Kern kernel, uint32_
   }
   hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(zk::kBlock), 0, c->stream, p.a, p.b, 0, args...);
   HIPCK(hipGetLastError());
+  if (c->work_open) {
+    c->stats.host_work_us +=
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->work_t0).count();
+    c->work_open = false;
+  }
   if (timed) c->pending.push_back(p);
   c->stats.launches[kind] += 1;
   c->stats.alg_bytes[kind] += bytes;
@@ -273,6 +283,7 @@ void flush_timing(zk_ctx* c) {
   c->pending.clear();
 }
 void sync(zk_ctx* c) {
+  c->work_open = false;
   HIPCK(hipStreamSynchronize(c->stream));
   c->stats.host_syncs += 1;
   flush_timing(c);
@@ -330,6 +341,7 @@ zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   zk::RoundSink s;
   s.partials = c->partials.fe();
   s.counter = d_counter(c);
+  s.accum = d_accum(c);
   s.tag = ++c->tag;
   const bool via_rccl = across_ranks && multi_rank(c) && c->comm == COMM_RCCL;
   s.dev_out = via_rccl ? d_red(c) : nullptr;
@@ -342,6 +354,10 @@ void wait_flag(zk_ctx* c, uint32_t tag) {
   const uint32_t* f = h_flag(c);
   uint64_t spins = 0;
   const auto t0 = std::chrono::steady_clock::now();
+  if (c->work_open) {  // host work since the previous result ends at this wait
+    c->stats.host_work_us += std::chrono::duration<double, std::micro>(t0 - c->work_t0).count();
+    c->work_open = false;
+  }
   while (__atomic_load_n(f, __ATOMIC_ACQUIRE) != tag) {
     __builtin_ia32_pause();
     if ((++spins & 0xFFFF) == 0) {
@@ -351,6 +367,9 @@ void wait_flag(zk_ctx* c, uint32_t tag) {
       if ((e == hipSuccess && s > 1.0) || s > 60.0) fail(ZK_EDEVICE, "round result flag never arrived");
     }
   }
+  c->work_t0 = std::chrono::steady_clock::now();
+  c->work_open = true;
+  c->stats.host_wait_us += std::chrono::duration<double, std::micro>(c->work_t0 - t0).count();
   c->stats.host_syncs += 1;
 }
 
@@ -373,7 +392,7 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, Fe (&ou
   for (int k = 0; k < K; ++k) out[k] = from_limb_sums<F>(w + 8 * k);
 }
 
-void ensure_partials(zk_ctx* c) { c->partials.ensure((size_t)c->num_cus * 8 * 4 * 32); }
+void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * 4 * 32); }
 
 // ---------------------------------------------------------------------------
 // GKR sum-check rounds

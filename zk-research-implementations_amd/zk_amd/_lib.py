@@ -33,6 +33,8 @@ class ZkStats(C.Structure):
         ("field_muls", C.c_double * 7),
         ("host_syncs", C.c_uint64),
         ("collectives", C.c_uint64),
+        ("host_wait_us", C.c_double),
+        ("host_work_us", C.c_double),
     ]
 
 
@@ -87,6 +89,16 @@ def lib():
                 f"{LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
                 "(or __graft_entry__.build()); the prover has no CPU fallback"
             )
+        # One HIP runtime per process: torch's libtorch_hip NEEDs the unversioned
+        # libamdhip64.so / librccl.so from its own lib dir, which the loader does not
+        # match against an already-loaded /opt/rocm libamdhip64.so.7, so loading us
+        # first and torch later leaves two runtimes that double-free at exit. Load
+        # torch's copies first; our NEEDED sonames (libamdhip64.so.7, librccl.so.1)
+        # then bind to them.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

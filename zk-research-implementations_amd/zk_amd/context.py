@@ -62,6 +62,8 @@ class Context:
             },
             "host_syncs": int(s.host_syncs),
             "collectives": int(s.collectives),
+            "host_wait_us": float(s.host_wait_us),
+            "host_work_us": float(s.host_work_us),
         }
 
     # ---- device tables ----
