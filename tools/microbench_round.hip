@@ -95,10 +95,10 @@ int main() {
 
   // the production kernels across round sizes, with the full epilogue
   // (two-level fan-in + publish to pinned host memory); back-to-back launches
-  Fe* parts;
+  uint64_t* parts;
   uint32_t* ctr;
   uint64_t* hout;
-  CK(hipMalloc(&parts, (256 * 8 + 8) * 4 * 32));
+  CK(hipMalloc(&parts, (256 * 8 + 8) * kSlotU64 * 8));
   CK(hipMalloc(&ctr, 4096));
   CK(hipMemset(ctr, 0, 4096));
   CK(hipHostMalloc(&hout, 4096, hipHostMallocMapped | hipHostMallocCoherent));

@@ -284,6 +284,32 @@ ZK_HD Fe wide_redc(const Wide& V) {
   return fe_add<F>(lo, fe_mul<F>(hi, r2));  // hi * R mod p
 }
 
+// Limb sums -> field element. w[i] (i < L <= 17) are sums of 32-bit words at
+// weight 2^(32 i) (each < 2^62), i.e. the integer T = sum_i w[i] 2^(32 i) < 2^624.
+// Split T = C0 + C1 R + C2 R^2 (R = 2^256).
+//   product sums (sums of a*b over Montgomery images, T ~ R^2 x):  T R^-1 = C0 R^-1 + C1 + C2 R
+//   element sums (sums of Montgomery images, T ~ R x):            T      = C0 + C1 R          (C2 = 0)
+template <class F>
+ZK_HD Fe limbs_to_fe(const uint64_t* w, int L, bool product) {
+  uint32_t t[24];
+  uint64_t carry = 0;
+  for (int i = 0; i < 24; ++i) {
+    const uint64_t s = (i < L ? w[i] : 0) + carry;
+    t[i] = (uint32_t)s;
+    carry = s >> 32;
+  }
+  Fe ch[3];
+  for (int c = 0; c < 3; ++c) {
+    for (int k = 0; k < 8; ++k) ch[c].v[k] = t[8 * c + k];
+    for (int k = 0; k < 5; ++k) ch[c] = fe_reduce_once<F>(ch[c]);  // 2^256 < 6p
+  }
+  Fe r2, one = fe_zero<F>();
+  for (int k = 0; k < 8; ++k) r2.v[k] = F::R2[k];
+  one.v[0] = 1;
+  if (product) return fe_add<F>(fe_add<F>(fe_mul<F>(ch[0], one), ch[1]), fe_mul<F>(ch[2], r2));
+  return fe_add<F>(ch[0], fe_mul<F>(ch[1], r2));
+}
+
 template <class F>
 ZK_HD Fe fe_to_mont(const Fe& canon) {  // canon < p
   Fe r2;

@@ -39,253 +39,203 @@ __device__ __forceinline__ Fe at2(const Fe& lo, const Fe& hi) {
   return fe_sub<F>(fe_dbl<F>(hi), lo);
 }
 
-// Where a round kernel's K partial sums go. Every block publishes its
-// partial with write-through (sc1) 8-byte stores, drains them, and one lane
-// bumps an agent-scope counter; the block whose add returns gridDim-1 reads
-// all partials back with sc1 loads (MI355X_MICROARCH.md "Valid forms", first
-// row of the sc1 hand-off table: no release/acquire fence, so the dirty L2
-// full of freshly folded table lines is never written back mid-kernel). It
-// writes the K totals limb-split (one u64 per 32-bit limb — the form the
-// multi-GPU all-reduce sums exactly) to dev_out and/or pinned host memory and
-// raises host_flag = tag with a system-scope release; the host spins on that
-// flag instead of synchronising the stream.
+// Where a round kernel's sums go. Everything after the main loop is integer
+// work: a thread's accumulators (17-word unreduced product sums `Wide`, or
+// 8-word element sums `Fe`) are summed over the block column by column
+// (one u64 per 32-bit word: "limb sums", exact, no carries, no reduction mod
+// p) through an LDS transpose, then over the grid, and the C = K*L limb sums
+// are handed over as they are. The consumer (host: limbs_to_fe) does the one
+// carry propagation + REDC. The multi-GPU all-reduce sums the same u64 vector.
+//
+// Cross-block fan-in: a single block publishes directly; up to
+// kAtomicFaninMax blocks add their limb sums with u64 atomics and count in;
+// larger grids meet in two levels (blockIdx % 8 shards, then a top counter)
+// through per-block slots written/read with write-through (sc1) 8-byte
+// accesses (MI355X_MICROARCH.md "Valid forms": no release/acquire fence, so
+// the dirty L2 full of freshly folded table lines is never written back
+// mid-kernel). The last block writes the totals to dev_out and/or pinned host
+// memory and raises host_flag = tag; the host spins on that flag instead of
+// synchronising the stream.
+//
+// Phase timestamps for tools/microbench_phases.hip (compile-time, off in the
+// library): block b writes s_memrealtime (100 MHz, device-global) into
+// zk_phase_trace[b * 8 + i] from thread 0.
+#ifdef ZK_PHASE_TRACE
+#define ZK_STAMP(i) \
+  do { if (threadIdx.x == 0) zk_phase_trace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define ZK_STAMP(i) do { } while (0)
+#endif
+
+constexpr int kSlotU64 = 64;  // per-block partial slot: up to 64 limb sums (512 B)
+
 struct RoundSink {
-  Fe* partials;         // [gridDim.x + 8][4]: one 128-B slot per block, then 8 shard slots
+  uint64_t* partials;   // [gridDim.x + 8][kSlotU64]: one slot per block, then 8 shard slots
   uint32_t* counter;    // 9 counters, 128 B apart: 8 XCD shards + top; zero at launch, reset by their last user
-  uint64_t* accum;      // K*8 u64 limb-split accumulator (small grids); zero at launch, reset by the last block
-  uint64_t* dev_out;    // K*8 u64 in device memory, or null
-  uint64_t* host_out;   // K*8 u64 in pinned host memory, or null
+  uint64_t* accum;      // C u64 accumulator (small grids); zero at launch, reset by the last block
+  uint64_t* dev_out;    // C u64 in device memory, or null
+  uint64_t* host_out;   // C u64 in pinned host memory, or null
   uint32_t* host_flag;  // pinned host word, or null
   uint32_t tag;
 };
 
-__device__ __forceinline__ void st_fe_sc1(Fe* p, uint64_t i, const Fe& x) {
-  uint64_t* q = reinterpret_cast<uint64_t*>(p + i);
-#pragma unroll
-  for (int w = 0; w < 4; ++w)
-    __hip_atomic_store(q + w, (uint64_t)x.v[2 * w] | ((uint64_t)x.v[2 * w + 1] << 32), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void st_u64_sc1(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ Fe ld_fe_sc1(Fe* p, uint64_t i) {
-  uint64_t* q = reinterpret_cast<uint64_t*>(p + i);
-  Fe x;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const uint64_t v = __hip_atomic_load(q + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    x.v[2 * w] = (uint32_t)v;
-    x.v[2 * w + 1] = (uint32_t)(v >> 32);
-  }
-  return x;
+__device__ __forceinline__ uint64_t ld_u64_sc1(uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Block-level sums use plain 288-bit integer adds (9 words, no modular
-// reduction per step): 256 values < p sum to < 2^264. One reduction mod p at
-// the end (lo256 mod p + hi * 2^256 mod p).
-struct W9 {
-  uint32_t w[9];
+// Shared scratch of the epilogue (one instance per kernel).
+template <int L>
+struct LimbScratch {
+  static constexpr int S = L | 1;  // odd row stride: conflict-free column reads
+  uint32_t rows[kBlock * S];
+  uint64_t part[4 * L];
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
 };
-__device__ __forceinline__ void w9_add(W9& a, const W9& b) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) a.w[i] = addc32(a.w[i], b.w[i], c, &c);
-}
-template <class F>
-__device__ __forceinline__ Fe w9_reduce(const W9& a) {
-  Fe lo;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) lo.v[i] = a.w[i];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) lo = fe_reduce_once<F>(lo);  // 2^256 < 6p
-  if (a.w[8] == 0) return lo;
-  Fe hi = fe_zero<F>(), r2;
-  hi.v[0] = a.w[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) r2.v[i] = F::R2[i];
-  return fe_add<F>(lo, fe_mul<F>(hi, r2));  // hi * 2^256 mod p
-}
 
-// sum K elements over the workgroup; the result is valid in threads 0..K-1
-template <class F, int K>
-__device__ __forceinline__ Fe block_sum(const Fe (&acc)[K], W9 (&sm)[kBlock / 64][K]) {
-  W9 v[K];
+// Column sums of one L-word value per thread over the block -> sc.tot[base + c].
+template <int L, class Sc>
+__device__ __forceinline__ void block_limb_sums(const uint32_t (&v)[L], Sc& sc, int base) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[k].w[i] = acc[k].v[i];
-    v[k].w[8] = 0;
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      W9 o;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) o.w[i] = __shfl_xor(v[k].w[i], off, 64);
-      w9_add(v[k], o);
-    }
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) sm[wave][k] = v[k];
+  for (int i = 0; i < L; ++i) sc.rows[t * Sc::S + i] = v[i];
+  __syncthreads();
+  if (lane < (uint32_t)L) {
+    uint64_t s = 0;
+    const uint32_t* col = sc.rows + wave * 64u * Sc::S + lane;
+#pragma unroll 16
+    for (int r = 0; r < 64; ++r) s += col[r * Sc::S];
+    sc.part[wave * L + lane] = s;
   }
   __syncthreads();
-  Fe s = fe_zero<F>();
-  if (threadIdx.x < K) {
-    W9 t = sm[0][threadIdx.x];
-#pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) w9_add(t, sm[w][threadIdx.x]);
-    s = w9_reduce<F>(t);
-  }
-  return s;
+  if (t < (uint32_t)L) sc.tot[base + t] = sc.part[t] + sc.part[L + t] + sc.part[2 * L + t] + sc.part[3 * L + t];
+}
+template <class Sc>
+__device__ __forceinline__ void block_limb_sums(const Wide& w, Sc& sc, int base) {
+  block_limb_sums<17>(w.w, sc, base);
+}
+template <class Sc>
+__device__ __forceinline__ void block_limb_sums(const Fe& x, Sc& sc, int base) {
+  block_limb_sums<8>(x.v, sc, base);
 }
 
-// final K totals -> limb-split outputs + host flag
-template <int K>
-__device__ __forceinline__ void publish_totals(const Fe& t, const RoundSink& sk) {
-  if (threadIdx.x < K) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (sk.dev_out) sk.dev_out[threadIdx.x * 8 + i] = t.v[i];
-      if (sk.host_out) sk.host_out[threadIdx.x * 8 + i] = t.v[i];
-    }
+// sc.tot[0..C) (written by wave 0 lanes) -> dev_out / host_out + host flag.
+// Wave 0 only: its lanes store the host copy with system-scope (write-through,
+// sc0 sc1) stores — plain stores to the pinned page would sit in L2 — drain,
+// then lane 0 raises the flag. No L2 writeback (buffer_wbl2) is needed since
+// nothing the host reads was written with plain stores.
+template <int C, class Sc>
+__device__ __forceinline__ void publish_limbs(Sc& sc, const RoundSink& sk) {
+  if (threadIdx.x >= 64) return;
+  const uint32_t lane = threadIdx.x;
+  if (lane < (uint32_t)C) {
+    const uint64_t v = sc.tot[lane];
+    if (sk.dev_out) sk.dev_out[lane] = v;
+    if (sk.host_out) __hip_atomic_store(sk.host_out + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0 && sk.host_flag) __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// sum `count` slots (slot index first + i*stride) of C limb sums -> sc.tot (wave 0 lanes)
+template <int C, class Sc>
+__device__ __forceinline__ void sum_slots(uint64_t* slots, uint32_t first, uint32_t stride, uint32_t count, Sc& sc) {
+  constexpr uint32_t P = kBlock / C;  // parts per column
+  const uint32_t t = threadIdx.x, c = t % C, p = t / C;
+  uint64_t s = 0;
+  if (p < P)
+    for (uint32_t i = p; i < count; i += P) s += ld_u64_sc1(slots + (uint64_t)(first + i * stride) * kSlotU64 + c);
+  sc.pp[t] = s;
   __syncthreads();
-  if (threadIdx.x == 0 && sk.host_flag) {
-    __threadfence_system();
-    __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < (uint32_t)C) {
+    uint64_t tot = 0;
+    for (uint32_t q = 0; q < P; ++q) tot += sc.pp[q * C + t];
+    sc.tot[t] = tot;
   }
 }
 
-// sum slots [first, first + count*stride) of `slots` (sc1 loads), spread over the block
-template <class F, int K>
-__device__ __forceinline__ Fe sum_slots(Fe* slots, uint32_t first, uint32_t stride, uint32_t count,
-                                        W9 (&sm)[kBlock / 64][K]) {
-  W9 tot[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int i = 0; i < 9; ++i) tot[k].w[i] = 0;
-  for (uint32_t b = threadIdx.x; b < count; b += kBlock) {
-    Fe x[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) x[k] = ld_fe_sc1(slots, (uint64_t)(first + b * stride) * 4 + k);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      W9 y;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) y.w[i] = x[k].v[i];
-      y.w[8] = 0;
-      w9_add(tot[k], y);
-    }
-  }
-  Fe red[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) red[k] = w9_reduce<F>(tot[k]);
-  __syncthreads();  // sm is reused
-  return block_sum<F, K>(red, sm);
-}
+constexpr uint32_t kAtomicFaninMax = 64;  // grids up to this size fan in through u64 atomics
 
-constexpr uint32_t kAtomicFaninMax = 64;  // grids up to this size fan in through limb atomics
-
-// Cross-block fan-in in two levels so no counter sees more than ~gridDim/8
-// arrivals (one device-scope counter serialises ~12 ns per arrival:
-// MI355X_MICROARCH.md "fanin"): blocks of shard s = blockIdx % 8 (one XCD
-// under round-robin placement — speed only, never correctness) meet on
-// counter s; each shard's last block sums the shard and meets the other
-// shards' last blocks on the top counter; the very last one publishes.
-template <class F, int K>
-__device__ __forceinline__ void block_reduce_finish(Fe (&acc)[K], const RoundSink& sk) {
-  __shared__ W9 sm[kBlock / 64][K];
-  __shared__ uint32_t am_last;
-  const Fe s = block_sum<F, K>(acc, sm);
-  const uint32_t G = gridDim.x;
-  if (G == 1) {  // single block: its sum is the total
-    publish_totals<K>(s, sk);
+// Block limb sums are in sc.tot[0..C) (valid for threads < C); finish over the grid.
+template <int C, class Sc>
+__device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk) {
+  static_assert(C <= kSlotU64 && C <= 64, "limb vector too long");
+  const uint32_t G = gridDim.x, t = threadIdx.x;
+  if (G == 1) {
+    ZK_STAMP(4);
+    ZK_STAMP(5);
+    publish_limbs<C>(sc, sk);
+    ZK_STAMP(6);
     return;
   }
   if (G <= kAtomicFaninMax) {
-    // Small grid: every block adds its K sums limb by limb (no-return u64
-    // atomics at the device-coherent level; G * 2^32 < 2^64 stays exact),
-    // drains, and counts in; the last block reads the totals with sc1 loads.
-    if (threadIdx.x < K) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        __hip_atomic_fetch_add(sk.accum + threadIdx.x * 8 + i, (uint64_t)s.v[i], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // every block adds its limb sums (no-return u64 atomics, device-coherent
+    // level; G * 256 * 2^32 < 2^64 stays exact), drains, and counts in
+    if (t < (uint32_t)C) __hip_atomic_fetch_add(sk.accum + t, sc.tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (t == 0) {
       const uint32_t prev = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      am_last = prev == G - 1;
+      sc.am_last = prev == G - 1;
     }
     __syncthreads();
-    if (!am_last) return;
+    ZK_STAMP(4);
+    if (!sc.am_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    Fe t = fe_zero<F>();
-    if (threadIdx.x < K) {
-      uint64_t w[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        w[i] = __hip_atomic_exchange(sk.accum + threadIdx.x * 8 + i, (uint64_t)0, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);  // read and re-arm for the next launch
-      W9 y;
-      uint64_t c = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint64_t v = w[i] + c;
-        y.w[i] = (uint32_t)v;
-        c = v >> 32;
-      }
-      y.w[8] = (uint32_t)c;
-      t = w9_reduce<F>(y);
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    publish_totals<K>(t, sk);
+    if (t < (uint32_t)C)  // read and re-arm for the next launch
+      sc.tot[t] = __hip_atomic_exchange(sk.accum + t, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ZK_STAMP(5);
+    publish_limbs<C>(sc, sk);
+    ZK_STAMP(6);
     return;
   }
   const uint32_t shard = blockIdx.x & 7u, nshards = G < 8 ? G : 8u;
   const uint32_t in_shard = (G - shard + 7u) / 8u;
-  if (threadIdx.x < K) st_fe_sc1(sk.partials, (uint64_t)blockIdx.x * 4 + threadIdx.x, s);
+  if (t < (uint32_t)C) st_u64_sc1(sk.partials + (uint64_t)blockIdx.x * kSlotU64 + t, sc.tot[t]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains before the signal
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     const uint32_t prev =
         __hip_atomic_fetch_add(sk.counter + 32 * shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    am_last = prev == in_shard - 1;
+    sc.am_last = prev == in_shard - 1;
   }
   __syncthreads();
-  if (!am_last) return;
+  ZK_STAMP(4);
+  if (!sc.am_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
-  const Fe ts = sum_slots<F, K>(sk.partials, shard, 8u, in_shard, sm);
-  if (threadIdx.x < K) st_fe_sc1(sk.partials, (uint64_t)(G + shard) * 4 + threadIdx.x, ts);
+  sum_slots<C>(sk.partials, shard, 8u, in_shard, sc);
+  if (t < (uint32_t)C) st_u64_sc1(sk.partials + (uint64_t)(G + shard) * kSlotU64 + t, sc.tot[t]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     __hip_atomic_store(sk.counter + 32 * shard, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     const uint32_t prev = __hip_atomic_fetch_add(sk.counter + 32 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    am_last = prev == nshards - 1;
+    sc.am_last = prev == nshards - 1;
   }
   __syncthreads();
-  if (!am_last) return;
+  if (!sc.am_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const Fe t = sum_slots<F, K>(sk.partials, G, 1u, nshards, sm);
-  if (threadIdx.x == 0) __hip_atomic_store(sk.counter + 32 * 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  publish_totals<K>(t, sk);
+  __syncthreads();  // pp is reused
+  sum_slots<C>(sk.partials, G, 1u, nshards, sc);
+  if (t == 0) __hip_atomic_store(sk.counter + 32 * 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ZK_STAMP(5);
+  publish_limbs<C>(sc, sk);
+  ZK_STAMP(6);
 }
 
-// copy K*8 u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
+// copy n u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
 __global__ void k_publish(const uint64_t* __restrict__ src, int n, uint64_t* host_out, uint32_t* host_flag,
                           uint32_t tag) {
-  if (threadIdx.x < n) host_out[threadIdx.x] = src[threadIdx.x];
+  if (threadIdx.x < n)
+    __hip_atomic_store(host_out + threadIdx.x, src[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    __hip_atomic_store(host_flag, tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (threadIdx.x == 0) __hip_atomic_store(host_flag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -321,8 +271,15 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round0(const Fe* __restrict__ A,
     wide_mac<F>(w1, x1, z1);
     wide_mac<F>(w2, at2<F>(x0, x1), at2<F>(z0, z1));
   }
-  Fe acc[3] = {wide_redc<F>(w0), wide_redc<F>(w1), wide_redc<F>(w2)};
-  block_reduce_finish<F, 3>(acc, sink);
+  ZK_STAMP(1);
+  ZK_STAMP(2);
+  __shared__ LimbScratch<17> sc;
+  block_limb_sums(w0, sc, 0);
+  block_limb_sums(w1, sc, 17);
+  block_limb_sums(w2, sc, 34);
+  __syncthreads();
+  ZK_STAMP(3);
+  grid_finish<51>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------
@@ -348,6 +305,7 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2,
                                                       Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h, Fe r,
                                                       RoundSink sink) {
+  ZK_STAMP(0);
   Wide w0 = wide_zero<F>(), w2 = wide_zero<F>();
   uint64_t j, step;
   uint32_t q;
@@ -371,8 +329,14 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
     wide_mac<F>(w0, a0, s0);
     wide_mac<F>(w2, at2<F>(a0, a1), at2<F>(s0, s1));
   }
-  Fe acc[2] = {wide_redc<F>(w0), wide_redc<F>(w2)};
-  block_reduce_finish<F, 2>(acc, sink);
+  ZK_STAMP(1);
+  ZK_STAMP(2);
+  __shared__ LimbScratch<17> sc;
+  block_limb_sums(w0, sc, 0);
+  block_limb_sums(w2, sc, 17);
+  __syncthreads();
+  ZK_STAMP(3);
+  grid_finish<34>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------
@@ -380,7 +344,8 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
 // latency-bound (one wave serialises 12 dependent 256-bit multiplies). Here 8
 // lanes share a pair: lane s folds table s>>1, half s&1 (one multiply); odd
 // lanes turn (lo, hi) into X(2) = 2 hi - lo; lanes {0,1,4,5} multiply with lane
-// s+2 (A*S / M*P at t = 0 and t = 2). Critical path: 2 multiplies.
+// s+2 (A*S / M*P at t = 0 and t = 2), accumulated unreduced. Critical path:
+// one multiply + one unreduced product.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ Fe shfl_fe(const Fe& x, int src) {
   Fe r;
@@ -394,10 +359,11 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict
                                                             Fe* __restrict__ A2, Fe* __restrict__ S2,
                                                             Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h,
                                                             Fe r, RoundSink sink) {
+  ZK_STAMP(0);
   const uint32_t lane = threadIdx.x & 63, s = threadIdx.x & 7, tb = s >> 1, half = s & 1;
   const Fe* __restrict__ X = tb == 0 ? A : tb == 1 ? S : tb == 2 ? M : P;
   Fe* __restrict__ Y = tb == 0 ? A2 : tb == 1 ? S2 : tb == 2 ? M2 : P2;
-  Fe acc[2] = {fe_zero<F>(), fe_zero<F>()};
+  Wide acc = wide_zero<F>();  // lanes 0,4: t = 0 products; lanes 1,5: t = 2; others unused
   const uint64_t stride = (uint64_t)gridDim.x * (kBlock / 8);
   // the loop bound is uniform per 8-lane group (and per wave: 8 groups share j's stride)
   for (uint64_t j = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 3; j < h; j += stride) {
@@ -407,11 +373,18 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict
     const Fe lo = shfl_fe(f, (int)(lane & ~1u));        // the group's lo for this table
     const Fe v = half ? at2<F>(lo, f) : f;               // even: X(0), odd: X(2)
     const Fe partner = shfl_fe(v, (int)((lane + 2) & 63));
-    const Fe prod = fe_mul<F>(v, partner);
-    if (s == 0 || s == 4) acc[0] = fe_add<F>(acc[0], prod);
-    if (s == 1 || s == 5) acc[1] = fe_add<F>(acc[1], prod);
+    wide_mac<F>(acc, v, partner);
   }
-  block_reduce_finish<F, 2>(acc, sink);
+  ZK_STAMP(1);
+  ZK_STAMP(2);
+  __shared__ LimbScratch<17> sc;
+  const bool mine = (s & 2u) == 0;  // s in {0, 1, 4, 5}
+  const Wide z = wide_zero<F>();
+  block_limb_sums(mine && half == 0 ? acc : z, sc, 0);
+  block_limb_sums(mine && half == 1 ? acc : z, sc, 17);
+  __syncthreads();
+  ZK_STAMP(3);
+  grid_finish<34>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------
@@ -438,7 +411,11 @@ __global__ __launch_bounds__(kBlock) void k_sc_round(const Fe* __restrict__ X, F
       acc[1] = fe_add<F>(acc[1], f1);
     }
   }
-  block_reduce_finish<F, 2>(acc, sink);
+  __shared__ LimbScratch<8> sc;
+  block_limb_sums(acc[0], sc, 0);
+  block_limb_sums(acc[1], sc, 8);
+  __syncthreads();
+  grid_finish<16>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------

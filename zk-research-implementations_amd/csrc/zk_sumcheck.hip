@@ -183,8 +183,8 @@ struct zk_ctx {
   DevBuf work[2];  // ping-pong fold workspaces: 4 tables each
   DevBuf input;    // host-API staging (4 tables)
   DevBuf partials;
-  DevBuf small;    // reduce output (u64[32]) + flag + gather buffers
-  uint64_t* h_red = nullptr;  // pinned, device-mapped: round sums (u64[32]) + flag word at [64]
+  DevBuf small;    // round totals (<= 64 u64) + flag + gather buffers
+  uint64_t* h_red = nullptr;  // pinned, device-mapped: round totals (<= 51 u64) + flag word at [64]
   uint32_t tag = 0;           // last round tag handed to a kernel
   uint64_t lanes_max_pairs = 1u << 15;  // rounds with <= this many pairs use 8 lanes per pair
   std::chrono::steady_clock::time_point work_t0;  // when the last round result was seen
@@ -208,7 +208,7 @@ struct zk_ctx {
 
 namespace {
 // small device area: [0,512) round sums, [512] input check flag, [1024,2304)
-// fan-in counters (9 x 128 B), [2560,2816) limb accumulator (<= 3 x 8 u64),
+// fan-in counters (9 x 128 B), [2560,3072) limb accumulator (<= 64 u64),
 // [4096, +64 KiB) all-reduce bounce buffer
 // (<= 256 ranks x 256 B), then the tail's 4 local elements and the gathered
 // 4 x world tables
@@ -289,27 +289,11 @@ void sync(zk_ctx* c) {
   flush_timing(c);
 }
 
-// limb-split sum (8 x u64 holding 32-bit limbs, possibly summed over ranks)
-// -> field element: lo256 mod p + hi * 2^256 mod p.
+// limb-split element sum (8 x u64 holding 32-bit limbs, possibly summed over
+// ranks) -> field element (Montgomery image of the sum)
 template <class F>
 Fe from_limb_sums(const uint64_t* w) {
-  uint32_t v[9];
-  uint64_t carry = 0;
-  for (int i = 0; i < 8; ++i) {
-    const uint64_t s = w[i] + carry;
-    v[i] = (uint32_t)s;
-    carry = s >> 32;
-  }
-  v[8] = (uint32_t)carry;
-  Fe lo;
-  memcpy(lo.v, v, 32);
-  for (int i = 0; i < 5; ++i) lo = zk::fe_reduce_once<F>(lo);
-  if (v[8] == 0) return lo;
-  Fe hi = zk::fe_zero<F>();
-  hi.v[0] = v[8];
-  Fe r2;
-  for (int i = 0; i < 8; ++i) r2.v[i] = F::R2[i];
-  return zk::fe_add<F>(lo, zk::fe_mul<F>(hi, r2));  // hi * R mod p
+  return zk::limbs_to_fe<F>(w, 8, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -339,7 +323,7 @@ void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
 
 zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   zk::RoundSink s;
-  s.partials = c->partials.fe();
+  s.partials = reinterpret_cast<uint64_t*>(c->partials.p);
   s.counter = d_counter(c);
   s.accum = d_accum(c);
   s.tag = ++c->tag;
@@ -373,26 +357,29 @@ void wait_flag(zk_ctx* c, uint32_t tag) {
   c->stats.host_syncs += 1;
 }
 
+// The round kernel's totals: K values of L limb sums each (L = 17: unreduced
+// product sums, L = 8: element sums), summed over ranks when sharded.
 template <class F, int K>
-void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, Fe (&out)[K]) {
+void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
   const bool multi = across_ranks && multi_rank(c);
+  const int n = K * L;
   if (multi && c->comm == COMM_RCCL) {
-    NCCLCK(ncclAllReduce(d_red(c), d_red(c), K * 8, ncclUint64, ncclSum, c->nccl, c->stream));
+    NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
     c->stats.collectives += 1;
-    zk::k_publish<<<1, 64, 0, c->stream>>>(d_red(c), K * 8, c->h_red, h_flag(c), sk.tag);
+    zk::k_publish<<<1, 64, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
     HIPCK(hipGetLastError());
   }
   wait_flag(c, sk.tag);
-  uint64_t w[K * 8];
-  for (int i = 0; i < K * 8; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
+  uint64_t w[K * 17];
+  for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
   if (multi && c->comm == COMM_HOST) {
-    if (c->ar(c->user, w, K * 8) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+    if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
     c->stats.collectives += 1;
   }
-  for (int k = 0; k < K; ++k) out[k] = from_limb_sums<F>(w + 8 * k);
+  for (int k = 0; k < K; ++k) out[k] = zk::limbs_to_fe<F>(w + L * k, L, L == 17);
 }
 
-void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * 4 * 32); }
+void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kSlotU64 * 8); }
 
 // ---------------------------------------------------------------------------
 // GKR sum-check rounds
@@ -443,7 +430,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       const zk::RoundSink sk = make_sink(c, across_ranks);
       launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, zk::k_gkr_round0<F>, grid, cur[0], cur[1], cur[2], cur[3], h, sk);
       Fe s[3];
-      collect_sums<F, 3>(c, sk, across_ranks, s);
+      collect_sums<F, 3>(c, sk, across_ranks, 17, s);
       e0 = s[0];
       e1 = s[1];
       e2 = s[2];
@@ -463,7 +450,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       }
       for (int t = 0; t < 4; ++t) cur[t] = nx[t];
       Fe s[2];
-      collect_sums<F, 2>(c, sk, across_ranks, s);
+      collect_sums<F, 2>(c, sk, across_ranks, 17, s);
       e0 = s[0];
       e2 = s[1];
       // s_{k-1}(X) = sum_j f(X, j) is exact (degree 2 in X), so
@@ -552,7 +539,7 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
   launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, zk::k_sc_round<F, true>, grid, dX, nullptr, h, zk::fe_zero<F>(), sk);
   tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps the GPU
   Fe s[2];
-  collect_sums<F, 2>(c, sk, false, s);
+  collect_sums<F, 2>(c, sk, false, 8, s);
   claimed = zk::fe_add<F>(s[0], s[1]);  // = sum of the table (:29)
   absorb<F>(tr, &claimed, 1);
   const Fe* cur = dX;
@@ -566,7 +553,7 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
       sk = make_sink(c, false);
       launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, zk::k_sc_round<F, false>, grid, cur, nx, h, rr, sk);
       cur = nx;
-      collect_sums<F, 2>(c, sk, false, s);
+      collect_sums<F, 2>(c, sk, false, 8, s);
     }
     rp[2 * k] = s[0];
     rp[2 * k + 1] = s[1];
