@@ -1,0 +1,80 @@
+"""Pre-enqueued rounds (default): every round kernel is enqueued before round
+0's sums are read and waits in-kernel for the host to post its challenge.
+
+* The proof is identical with and without pre-enqueue (ZK_PRELAUNCH=0 launches
+  each round after its challenge), and equal to the oracle's.
+* When the host fails mid-proof (here: the host all-reduce callback raises in
+  round 3), the call returns ZK_ECOMM promptly — the guard releases every
+  kernel still waiting instead of letting each run into its 1 s limit — and
+  the same context proves correctly afterwards.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+
+import numpy as np
+import pytest
+
+import coracle as co
+
+import zk_amd
+from zk_amd._lib import ZK_ECOMM, ZkError, check, lib
+from zk_amd.elems import as_limbs, ptr, to_ints
+
+pytestmark = pytest.mark.gpu
+
+
+def _prove(ctx, field: int, n: int) -> tuple[list, list]:
+    tabs = [ctx.synth(field, 1 << n, seed=23, table=t) for t in range(4)]
+    arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
+    coeffs = np.zeros((n, 3, 4), np.uint64)
+    nco = np.zeros(n, np.uint8)
+    ch = np.zeros((n, 4), np.uint64)
+    tr = zk_amd.Transcript(field)
+    check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, n, 0, ptr(as_limbs([0])), tr.h, ptr(coeffs),
+                                                  ptr(nco), ptr(ch)))
+    return [to_ints(coeffs[k, : nco[k]]) for k in range(n)], to_ints(ch)
+
+
+def _oracle(field: int, n: int) -> tuple[list, list]:
+    tabs = [co.synth(field, 23, t, 0, 1 << n) for t in range(4)]
+    polys, chal = co.gkr_prove(field, tabs, co.Transcript())
+    return [list(p) for p in polys], list(chal)
+
+
+@pytest.mark.parametrize("field", [0, 2])
+def test_prelaunch_and_per_round_launch_agree(monkeypatch, field):
+    n = 16
+    want = _oracle(field, n)
+    for mode in ("1", "0"):
+        monkeypatch.setenv("ZK_PRELAUNCH", mode)
+        ctx = zk_amd.Context(0)
+        try:
+            assert _prove(ctx, field, n) == want, f"ZK_PRELAUNCH={mode}"
+        finally:
+            ctx.close()
+
+
+def test_host_failure_mid_proof_releases_waiting_rounds(monkeypatch):
+    monkeypatch.setenv("ZK_FORCE_COLLECTIVES", "1")  # route every round through the host all-reduce at world 1
+    ctx = zk_amd.Context(0)
+    try:
+        calls = {"n": 0}
+
+        def failing(buf):  # identity at world 1, raises in round 3
+            calls["n"] += 1
+            if calls["n"] == 4:
+                raise RuntimeError("peer lost")
+
+        ctx.attach_host_comm(0, 1, failing)
+        t0 = time.perf_counter()
+        with pytest.raises(ZkError) as e:
+            _prove(ctx, 0, 18)
+        elapsed = time.perf_counter() - t0
+        assert e.value.code == ZK_ECOMM
+        assert elapsed < 0.5, f"waiting rounds were not released ({elapsed:.2f} s)"
+        ctx.attach_host_comm(0, 1, lambda buf: None)
+        assert _prove(ctx, 0, 14) == _oracle(0, 14)
+    finally:
+        ctx.close()

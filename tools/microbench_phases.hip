@@ -26,6 +26,8 @@ int main() {
   for (Fe* t : {A, S, M, P}) CK(hipMemset(t, 0x11, N * 32));
   Fe r;
   for (int i = 0; i < 8; ++i) r.v[i] = 0x01020304u * (i + 1) & 0x0fffffff;
+  RoundIn rin{};
+  rin.r = r;
   uint64_t* parts; uint32_t* ctr; uint64_t* hout; unsigned long long* tr;
   CK(hipMalloc(&parts, (256 * 8 + 8) * kSlotU64 * 8));
   CK(hipMalloc(&ctr, 4096)); CK(hipMemset(ctr, 0, 4096));
@@ -50,9 +52,9 @@ int main() {
       g = std::min<uint64_t>(g, (uint64_t)prop.multiProcessorCount * pc[lanes]);
       auto launch = [&] {
         if (lanes)
-          k_gkr_round_lanes<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, r, sk);
+          k_gkr_round_lanes<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, rin, sk);
         else
-          k_gkr_round<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, r, sk);
+          k_gkr_round<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, rin, sk);
       };
       for (int i = 0; i < 3; ++i) launch();
       CK(hipDeviceSynchronize());

@@ -69,6 +69,8 @@ int main() {
   for (Fe* t : {A, S, M, P}) CK(hipMemset(t, 0x11, N * 32));
   Fe r;
   for (int i = 0; i < 8; ++i) r.v[i] = 0x01020304u * (i + 1) & 0x0fffffff;
+  RoundIn rin{};
+  rin.r = r;
   int per_cu = 0;
   CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_round<F, 0>, kBlock, 0));
   hipDeviceProp_t prop;
@@ -118,9 +120,9 @@ int main() {
       if (g > cap) g = cap;
       auto launch = [&] {
         if (lanes == 1)
-          k_gkr_round_lanes<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, r, sk);
+          k_gkr_round_lanes<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, rin, sk);
         else
-          k_gkr_round<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, r, sk);
+          k_gkr_round<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, rin, sk);
       };
       launch();
       CK(hipDeviceSynchronize());

@@ -28,6 +28,29 @@ __device__ __forceinline__ void st_fe(Fe* __restrict__ p, uint64_t i, const Fe& 
   q[1] = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
 }
 
+// Folded-table stores. ZK_FOLD_STORE: 0 plain (write-back L2), 1 non-temporal
+// hint, 2 write-through (sc1) so the kernel does not end with the L2 full of
+// dirty table lines to write back.
+#ifndef ZK_FOLD_STORE
+#define ZK_FOLD_STORE 0
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_fold(Fe* __restrict__ p, uint64_t i, const Fe& x) {
+#if ZK_FOLD_STORE == 0
+  st_fe(p, i, x);
+#else
+  u32x4* q = reinterpret_cast<u32x4*>(p) + 2 * i;
+  const u32x4 a = {x.v[0], x.v[1], x.v[2], x.v[3]}, b = {x.v[4], x.v[5], x.v[6], x.v[7]};
+#if ZK_FOLD_STORE == 1
+  __builtin_nontemporal_store(a, q);
+  __builtin_nontemporal_store(b, q + 1);
+#else
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\tglobal_store_dwordx4 %0, %2, off offset:16 sc1"
+               :: "v"(q), "v"(a), "v"(b) : "memory");
+#endif
+#endif
+}
+
 // a + r (b - a)
 template <class F>
 __device__ __forceinline__ Fe fold1(const Fe& a, const Fe& b, const Fe& r) {
@@ -63,8 +86,17 @@ __device__ __forceinline__ Fe at2(const Fe& lo, const Fe& hi) {
 #ifdef ZK_PHASE_TRACE
 #define ZK_STAMP(i) \
   do { if (threadIdx.x == 0) zk_phase_trace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// ZK_STAMP_AFTER(i, w): stamp once the 17-word accumulator w is computed
+#define ZK_STAMP_AFTER(i, a_)                                         \
+  do {                                                                 \
+    uint32_t x_ = 0;                                                   \
+    for (int k_ = 0; k_ < 17; ++k_) x_ ^= (a_).w[k_];                  \
+    asm volatile("; stamp dep %0" ::"v"(x_));                          \
+    ZK_STAMP(i);                                                       \
+  } while (0)
 #else
 #define ZK_STAMP(i) do { } while (0)
+#define ZK_STAMP_AFTER(i, w) do { } while (0)
 #endif
 
 constexpr int kSlotU64 = 64;  // per-block partial slot: up to 64 limb sums (512 B)
@@ -79,6 +111,82 @@ struct RoundSink {
   uint32_t tag;
 };
 
+// ---------------------------------------------------------------------------
+// Pre-enqueued rounds. The host enqueues every round kernel up front; round
+// k's kernel starts as soon as round k-1's ends and waits, in-kernel, for the
+// host to post r_{k-1} (after reading round k-1's sums and running the
+// transcript). Only thread 0 of block 0 polls the pinned host slot: uncached
+// reads of one host address from several pollers serialise (~1.5 us each,
+// measured: 64 polling blocks added ~100 us to a round). Block 0 relays r
+// through a device word that the other blocks poll. Every wait gives up after
+// ~1 s and flags an error (the host then fails the call): no wave can spin
+// forever.
+// ---------------------------------------------------------------------------
+struct alignas(64) RWait {
+  Fe r;          // Montgomery
+  uint32_t tag;  // valid for every kernel expecting a tag <= this one (tags increase)
+  uint32_t pad[7];
+};
+struct RoundIn {
+  Fe r;                // used as is when host == null
+  const RWait* host;   // pinned slot the host posts r to, or null
+  RWait* relay;        // kRelays device relay slots (zeroed tags at rest), used when gridDim > 1
+  uint32_t* err;       // pinned error word
+  uint32_t tag;
+};
+constexpr uint64_t kWaitTicks = 100000000ull;  // 1 s of s_memrealtime (100 MHz)
+#ifndef ZK_RELAYS
+#define ZK_RELAYS 1
+#endif
+#ifndef ZK_RELAY_SLEEP
+#define ZK_RELAY_SLEEP 1
+#endif
+constexpr uint32_t kRelays = ZK_RELAYS;  // block b polls relay b % kRelays (1 measured best: 8 replicas cost block 0 more than they save)
+
+__device__ __forceinline__ Fe block_get_r(const RoundIn& in) {
+  if (!in.host) return in.r;
+  __shared__ Fe s_r;
+  if (threadIdx.x == 0) {
+    const bool direct = blockIdx.x == 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    Fe r;
+    if (direct) {
+      // relaxed system-scope polls: uncached (sc0 sc1) loads with no cache
+      // invalidate per iteration; the r loads below are uncached too and issue
+      // only after the tag has been seen
+      while ((int32_t)(__hip_atomic_load(&in.host->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - in.tag) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = false; break; }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r.v[i] = __hip_atomic_load(&in.host->r.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (gridDim.x > 1) {  // block 0 relays (write-through stores, drained before the tags)
+        const uint32_t nrel = gridDim.x < kRelays ? gridDim.x : kRelays;
+        for (uint32_t k = 0; k < nrel; ++k)
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            __hip_atomic_store(&in.relay[k].r.v[i], r.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (uint32_t k = 0; k < nrel; ++k)
+          __hip_atomic_store(&in.relay[k].tag, in.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      const RWait* rl = in.relay + blockIdx.x % kRelays;
+      while ((int32_t)(__hip_atomic_load(&rl->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - in.tag) < 0) {
+        __builtin_amdgcn_s_sleep(ZK_RELAY_SLEEP);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = false; break; }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r.v[i] = __hip_atomic_load(&rl->r.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!ok) __hip_atomic_store(in.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_r = r;
+  }
+  __syncthreads();
+  return s_r;
+}
+
 __device__ __forceinline__ void st_u64_sc1(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -91,28 +199,40 @@ template <int L>
 struct LimbScratch {
   static constexpr int S = L | 1;  // odd row stride: conflict-free column reads
   uint32_t rows[kBlock * S];
-  uint64_t part[4 * L];
   uint64_t tot[kSlotU64];
   uint64_t pp[kBlock];
   uint32_t am_last;
 };
 
-// Column sums of one L-word value per thread over the block -> sc.tot[base + c].
+// Column sums of one L-word value per thread over the block -> sc.tot[base + c]
+// (valid in threads < L after the call). Every thread then sums one column
+// over a strided group of rows (G = kBlock / L groups, ~kBlock / G rows each);
+// threads < L add the G group sums.
 template <int L, class Sc>
 __device__ __forceinline__ void block_limb_sums(const uint32_t (&v)[L], Sc& sc, int base) {
-  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  constexpr uint32_t G = kBlock / L;
+  const uint32_t t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < L; ++i) sc.rows[t * Sc::S + i] = v[i];
   __syncthreads();
-  if (lane < (uint32_t)L) {
-    uint64_t s = 0;
-    const uint32_t* col = sc.rows + wave * 64u * Sc::S + lane;
-#pragma unroll 16
-    for (int r = 0; r < 64; ++r) s += col[r * Sc::S];
-    sc.part[wave * L + lane] = s;
+  const uint32_t c = t % L, g = t / L;
+  uint64_t s0 = 0, s1 = 0;
+  if (g < G) {
+    uint32_t r = g;
+    for (; r + G < (uint32_t)kBlock; r += 2 * G) {
+      s0 += sc.rows[r * Sc::S + c];
+      s1 += sc.rows[(r + G) * Sc::S + c];
+    }
+    if (r < (uint32_t)kBlock) s0 += sc.rows[r * Sc::S + c];
   }
+  sc.pp[t] = s0 + s1;
   __syncthreads();
-  if (t < (uint32_t)L) sc.tot[base + t] = sc.part[t] + sc.part[L + t] + sc.part[2 * L + t] + sc.part[3 * L + t];
+  if (t < (uint32_t)L) {
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < G; ++q) tot += sc.pp[q * L + t];
+    sc.tot[base + t] = tot;
+  }
 }
 template <class Sc>
 __device__ __forceinline__ void block_limb_sums(const Wide& w, Sc& sc, int base) {
@@ -303,9 +423,10 @@ template <class F>
 __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2,
-                                                      Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h, Fe r,
-                                                      RoundSink sink) {
+                                                      Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h,
+                                                      RoundIn rin, RoundSink sink) {
   ZK_STAMP(0);
+  const Fe r = block_get_r(rin);
   Wide w0 = wide_zero<F>(), w2 = wide_zero<F>();
   uint64_t j, step;
   uint32_t q;
@@ -322,15 +443,15 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
 #endif
     const Fe a0 = fold1<F>(x0, x2, r), a1 = fold1<F>(x1, x3, r);
     const Fe s0 = fold1<F>(z0, z2, r), s1 = fold1<F>(z1, z3, r);
-    st_fe(X2, j, a0);
-    st_fe(X2, j + h, a1);
-    st_fe(Z2, j, s0);
-    st_fe(Z2, j + h, s1);
+    st_fold(X2, j, a0);
+    st_fold(X2, j + h, a1);
+    st_fold(Z2, j, s0);
+    st_fold(Z2, j + h, s1);
     wide_mac<F>(w0, a0, s0);
     wide_mac<F>(w2, at2<F>(a0, a1), at2<F>(s0, s1));
   }
-  ZK_STAMP(1);
-  ZK_STAMP(2);
+  ZK_STAMP_AFTER(1, w0);
+  ZK_STAMP_AFTER(2, w2);
   __shared__ LimbScratch<17> sc;
   block_limb_sums(w0, sc, 0);
   block_limb_sums(w2, sc, 17);
@@ -358,8 +479,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict
                                                             const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                             Fe* __restrict__ A2, Fe* __restrict__ S2,
                                                             Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h,
-                                                            Fe r, RoundSink sink) {
+                                                            RoundIn rin, RoundSink sink) {
   ZK_STAMP(0);
+  const Fe r = block_get_r(rin);
   const uint32_t lane = threadIdx.x & 63, s = threadIdx.x & 7, tb = s >> 1, half = s & 1;
   const Fe* __restrict__ X = tb == 0 ? A : tb == 1 ? S : tb == 2 ? M : P;
   Fe* __restrict__ Y = tb == 0 ? A2 : tb == 1 ? S2 : tb == 2 ? M2 : P2;
@@ -369,7 +491,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict
   for (uint64_t j = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 3; j < h; j += stride) {
     const uint64_t o = j + half * h;
     const Fe f = fold1<F>(ld_fe(X, o), ld_fe(X, o + 2 * h), r);
-    st_fe(Y, o, f);
+    st_fold(Y, o, f);
     const Fe lo = shfl_fe(f, (int)(lane & ~1u));        // the group's lo for this table
     const Fe v = half ? at2<F>(lo, f) : f;               // even: X(0), odd: X(2)
     const Fe partner = shfl_fe(v, (int)((lane + 2) & 63));
@@ -394,8 +516,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict
 //        the folded halves. out must not alias X.
 // ---------------------------------------------------------------------------
 template <class F, bool FIRST>
-__global__ __launch_bounds__(kBlock) void k_sc_round(const Fe* __restrict__ X, Fe* __restrict__ Y, uint64_t h, Fe r,
-                                                     RoundSink sink) {
+__global__ __launch_bounds__(kBlock) void k_sc_round(const Fe* __restrict__ X, Fe* __restrict__ Y, uint64_t h,
+                                                     RoundIn rin, RoundSink sink) {
+  const Fe r = FIRST ? rin.r : block_get_r(rin);
   Fe acc[2] = {fe_zero<F>(), fe_zero<F>()};
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < h; j += stride) {
@@ -405,8 +528,8 @@ __global__ __launch_bounds__(kBlock) void k_sc_round(const Fe* __restrict__ X, F
     } else {
       const Fe x0 = ld_fe(X, j), x1 = ld_fe(X, j + h), x2 = ld_fe(X, j + 2 * h), x3 = ld_fe(X, j + 3 * h);
       const Fe f0 = fold1<F>(x0, x2, r), f1 = fold1<F>(x1, x3, r);
-      st_fe(Y, j, f0);
-      st_fe(Y, j + h, f1);
+      st_fold(Y, j, f0);
+      st_fold(Y, j + h, f1);
       acc[0] = fe_add<F>(acc[0], f0);
       acc[1] = fe_add<F>(acc[1], f1);
     }

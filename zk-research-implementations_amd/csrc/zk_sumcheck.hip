@@ -202,6 +202,8 @@ struct zk_ctx {
   CommKind comm = COMM_NONE;
   zk_allreduce_u64_fn ar = nullptr;
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
+  bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
+  uint32_t rtag = 0;        // last tag handed to a pre-enqueued round kernel
   void* user = nullptr;
   ncclComm_t nccl = nullptr;
 };
@@ -219,6 +221,12 @@ uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_
 uint64_t* d_accum(zk_ctx* c) { return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(c->small.p) + 2560); }
 uint32_t* h_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(c->h_red + 64); }
 char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 4096; }
+// pre-enqueued rounds: the pinned slot the host posts r to, the pinned error
+// word, and the device relay slots (h_red page: [1024, 1088) and [2048];
+// small area: [3072, 3584) = 8 x 64 B)
+zk::RWait* h_rin(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->h_red) + 1024); }
+uint32_t* h_err(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->h_red) + 2048); }
+zk::RWait* d_relay(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->small.p) + 3072); }
 
 void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
 
@@ -274,9 +282,11 @@ void launch(zk_ctx* c, int kind, double bytes, double muls, Kern kernel, uint32_
 }
 // after a stream sync: fold event timings into the stats
 void flush_timing(zk_ctx* c) {
+  static const bool dbg = getenv("ZK_DEBUG_EVENTS") != nullptr;
   for (auto& p : c->pending) {
     float ms = 0.f;
     HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
+    if (dbg) fprintf(stderr, "zk: kind %d %.1f us\n", p.kind, ms * 1e3);
     c->stats.kernel_ms[p.kind] += ms;
     c->ev_free.push_back({p.a, p.b});
   }
@@ -359,17 +369,24 @@ void wait_flag(zk_ctx* c, uint32_t tag) {
 
 // The round kernel's totals: K values of L limb sums each (L = 17: unreduced
 // product sums, L = 8: element sums), summed over ranks when sharded.
-template <class F, int K>
-void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
-  const bool multi = across_ranks && multi_rank(c);
-  const int n = K * L;
-  if (multi && c->comm == COMM_RCCL) {
+// Stream side of a round's hand-off, enqueued right after its kernel: across
+// ranks over RCCL the device totals are all-reduced and then published.
+void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
+  if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
     NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
     c->stats.collectives += 1;
     zk::k_publish<<<1, 64, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
     HIPCK(hipGetLastError());
   }
+}
+
+template <class F, int K>
+void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
+  const bool multi = across_ranks && multi_rank(c);
+  const int n = K * L;
   wait_flag(c, sk.tag);
+  if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) != 0)
+    fail(ZK_EDEVICE, "a pre-enqueued round kernel waited more than 1 s for its challenge");
   uint64_t w[K * 17];
   for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
   if (multi && c->comm == COMM_HOST) {
@@ -412,45 +429,104 @@ Fe finish_round(zk_transcript* tr, const Fe& e0, const Fe& e1, const Fe& e2, uin
   return fe_add<F>(c[0], fe_mul<F>(r, fe_add<F>(c[1], fe_mul<F>(r, c[2]))));
 }
 
+// Posts the challenge of a finished round to the pinned slot the next
+// pre-enqueued round kernel polls. If the host unwinds mid-proof (exception),
+// the destructor posts the last tag (kernels compare with >=, so every round
+// still waiting proceeds with r = 0; its results are discarded) and drains
+// the stream, so no kernel is left waiting.
+struct PostR {
+  zk_ctx* c;
+  uint32_t last = 0;  // highest tag a kernel of this phase waits for (0: none)
+  bool done = false;
+  void post(const Fe& r, uint32_t tag) {
+    zk::RWait* s = h_rin(c);
+    for (int i = 0; i < 8; ++i) __atomic_store_n(&s->r.v[i], r.v[i], __ATOMIC_RELAXED);
+    __atomic_store_n(&s->tag, tag, __ATOMIC_RELEASE);
+  }
+  ~PostR() {
+    if (done || last == 0) return;
+    post(zk::fe_zero<zk::Bn254Fr>(), last);
+    (void)hipStreamSynchronize(c->stream);
+  }
+};
+
+// Pre-enqueue the rounds of a phase (ZK_PRELAUNCH, default on)?
+bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1; }
+
 // Run `nv` rounds over 4 device tables of 2^nv elements starting at global
 // round k0. The first round of a phase computes e0,e1,e2 directly; later
 // rounds fold by the previous challenge in the same kernel. On return `cur`
 // points at the (unfolded) size-2 tables of the last round.
+// Pre-enqueued (default): every round kernel (and, across ranks over RCCL,
+// its all-reduce + publish) is enqueued before round 0's sums are read;
+// round i's kernel waits in-kernel for r_{i-1}, which the host posts as soon
+// as it has run the transcript. Otherwise each round is launched after the
+// previous challenge is known.
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
                GkrOut& out, Fe& claim, Fe& r) {
   const uint64_t L = (uint64_t)1 << nv;
-  for (uint32_t i = 0; i < nv; ++i) {
-    const uint32_t k = k0 + i;
+  const bool pre = prelaunch(c, nv);
+  std::vector<zk::RoundSink> sinks(nv);
+  std::vector<uint32_t> rtags(nv, 0);
+  auto enqueue = [&](uint32_t i) {
     const uint64_t size = L >> i;  // table length in this round
     const uint64_t h = size / 2;   // pairs
-    Fe e0, e1, e2;
+    sinks[i] = make_sink(c, across_ranks);
+    const zk::RoundSink& sk = sinks[i];
     if (i == 0) {
       const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round0<F>);
-      const zk::RoundSink sk = make_sink(c, across_ranks);
       launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, zk::k_gkr_round0<F>, grid, cur[0], cur[1], cur[2], cur[3], h, sk);
+      enqueue_reduce(c, sk, across_ranks, 3 * 17);
+      return;
+    }
+    // fold previous (size 2*size) -> work[(i+1)&1] (size `size`) and evaluate;
+    // work[0] holds the size-L/2 level, work[1] the size-L/4 level, ...
+    Fe* w = c->work[(i + 1) & 1].fe();
+    Fe* nx[4] = {w, w + size, w + 2 * size, w + 3 * size};
+    zk::RoundIn rin{};
+    if (pre) {
+      rin.host = h_rin(c);
+      rin.relay = d_relay(c);
+      rin.err = h_err(c);
+      rin.tag = rtags[i] = ++c->rtag;
+    } else {
+      rin.r = r;
+    }
+    if (h <= c->lanes_max_pairs) {  // latency-bound size: 8 lanes per pair
+      const uint32_t g8 = grid_for(c, 8 * h, zk::k_gkr_round_lanes<F>);
+      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round_lanes<F>, g8, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
+    } else {
+      const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round<F>);
+      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
+    }
+    for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+    enqueue_reduce(c, sk, across_ranks, 2 * 17);
+  };
+  PostR post{c};
+  if (pre) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; i < nv; ++i) {
+      enqueue(i);
+      post.last = rtags[i];  // from here on the guard releases what is enqueued
+    }
+    if (getenv("ZK_DEBUG_ENQUEUE"))
+      fprintf(stderr, "zk: enqueued %u rounds in %.1f us\n", nv,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+  for (uint32_t i = 0; i < nv; ++i) {
+    const uint32_t k = k0 + i;
+    if (!pre) enqueue(i);
+    Fe e0, e1, e2;
+    if (i == 0) {
       Fe s[3];
-      collect_sums<F, 3>(c, sk, across_ranks, 17, s);
+      collect_sums<F, 3>(c, sinks[i], across_ranks, 17, s);
       e0 = s[0];
       e1 = s[1];
       e2 = s[2];
     } else {
-      const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round<F>);
-      // fold previous (size 2*size) -> work[(i+1)&1] (size `size`) and evaluate;
-      // work[0] holds the size-L/2 level, work[1] the size-L/4 level, ...
-      Fe* w = c->work[(i + 1) & 1].fe();
-      Fe* nx[4] = {w, w + size, w + 2 * size, w + 3 * size};
-      const Fe rr = r;
-      const zk::RoundSink sk = make_sink(c, across_ranks);
-      if (h <= c->lanes_max_pairs) {  // latency-bound size: 8 lanes per pair
-        const uint32_t g8 = grid_for(c, 8 * h, zk::k_gkr_round_lanes<F>);
-        launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round_lanes<F>, g8, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rr, sk);
-      } else {
-        launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rr, sk);
-      }
-      for (int t = 0; t < 4; ++t) cur[t] = nx[t];
       Fe s[2];
-      collect_sums<F, 2>(c, sk, across_ranks, 17, s);
+      collect_sums<F, 2>(c, sinks[i], across_ranks, 17, s);
       e0 = s[0];
       e2 = s[1];
       // s_{k-1}(X) = sum_j f(X, j) is exact (degree 2 in X), so
@@ -458,7 +534,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       e1 = zk::fe_sub<F>(claim, e0);
     }
     claim = finish_round<F>(tr, e0, e1, e2, k, out, r);
+    if (pre && i + 1 < nv) post.post(r, rtags[i + 1]);
   }
+  post.done = true;
 }
 
 template <class F>
@@ -472,6 +550,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   out.challenges.assign(n, zk::fe_zero<F>());
   if (n == 0) return;
   ensure_partials(c);
+  __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
   const uint64_t Lloc = (uint64_t)1 << nloc;
   const uint64_t wmax = std::max<uint64_t>(Lloc / 2, (uint64_t)G);
   c->work[0].ensure(4 * wmax * 32);
@@ -520,9 +599,10 @@ template <class F>
 void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, const uint8_t* table_bytes,
                      size_t nbytes, Fe* rp, Fe& claimed) {
   // The transcript absorbs the whole table first (sum_check_protocol.rs:27):
-  // a serial host Keccak. Round 0's half sums are launched before it so the
-  // GPU works underneath the hash.
+  // a serial host Keccak. Round 0's half sums (and, pre-enqueued, every later
+  // round) are launched before it so the GPU works underneath the hash.
   ensure_partials(c);
+  __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
   const uint64_t N = (uint64_t)1 << n;
   if (n == 0) {
     tr->h.update(table_bytes, nbytes);
@@ -533,33 +613,58 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
   }
   c->work[0].ensure(std::max<uint64_t>(N / 2, 1) * 32);
   c->work[1].ensure(std::max<uint64_t>(N / 4, 1) * 32);
-  uint64_t h = N / 2;
-  uint32_t grid = grid_for(c, h, zk::k_sc_round<F, true>);
-  zk::RoundSink sk = make_sink(c, false);
-  launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, zk::k_sc_round<F, true>, grid, dX, nullptr, h, zk::fe_zero<F>(), sk);
-  tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps the GPU
-  Fe s[2];
-  collect_sums<F, 2>(c, sk, false, 8, s);
-  claimed = zk::fe_add<F>(s[0], s[1]);  // = sum of the table (:29)
-  absorb<F>(tr, &claimed, 1);
+  const bool pre = prelaunch(c, n);
+  std::vector<zk::RoundSink> sinks(n);
+  std::vector<uint32_t> rtags(n, 0);
   const Fe* cur = dX;
   Fe r = zk::fe_zero<F>();
+  auto enqueue = [&](uint32_t k) {
+    sinks[k] = make_sink(c, false);
+    zk::RoundIn rin{};
+    if (k == 0) {
+      const uint64_t h = N / 2;
+      const uint32_t grid = grid_for(c, h, zk::k_sc_round<F, true>);
+      launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, zk::k_sc_round<F, true>, grid, dX, nullptr, h, rin, sinks[k]);
+      return;
+    }
+    const uint64_t h = (N >> k) / 2;
+    const uint32_t grid = grid_for(c, h, zk::k_sc_round<F, false>);
+    Fe* nx = c->work[(k + 1) & 1].fe();
+    if (pre) {
+      rin.host = h_rin(c);
+      rin.relay = d_relay(c);
+      rin.err = h_err(c);
+      rin.tag = rtags[k] = ++c->rtag;
+    } else {
+      rin.r = r;
+    }
+    launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, zk::k_sc_round<F, false>, grid, cur, nx, h, rin, sinks[k]);
+    cur = nx;
+  };
+  PostR post{c};
+  if (pre)
+    for (uint32_t k = 0; k < n; ++k) {
+      enqueue(k);
+      post.last = rtags[k];
+    }
+  else
+    enqueue(0);
+  tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps the GPU
   for (uint32_t k = 0; k < n; ++k) {
-    if (k > 0) {
-      h = (N >> k) / 2;
-      grid = grid_for(c, h, zk::k_sc_round<F, false>);
-      Fe* nx = c->work[(k + 1) & 1].fe();
-      const Fe rr = r;
-      sk = make_sink(c, false);
-      launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, zk::k_sc_round<F, false>, grid, cur, nx, h, rr, sk);
-      cur = nx;
-      collect_sums<F, 2>(c, sk, false, 8, s);
+    if (!pre && k > 0) enqueue(k);
+    Fe s[2];
+    collect_sums<F, 2>(c, sinks[k], false, 8, s);
+    if (k == 0) {
+      claimed = zk::fe_add<F>(s[0], s[1]);  // = sum of the table (:29)
+      absorb<F>(tr, &claimed, 1);
     }
     rp[2 * k] = s[0];
     rp[2 * k + 1] = s[1];
     absorb<F>(tr, s, 2);
     r = challenge<F>(tr);
+    if (pre && k + 1 < n) post.post(r, rtags[k + 1]);
   }
+  post.done = true;
   sync(c);
 }
 
@@ -668,6 +773,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     c->device = device;
     if (const char* e = getenv("ZK_LANES_MAX_PAIRS")) c->lanes_max_pairs = strtoull(e, nullptr, 0);  // tuning knob
     if (const char* e = getenv("ZK_FORCE_COLLECTIVES")) c->force_coll = atoi(e) != 0;
+    if (const char* e = getenv("ZK_PRELAUNCH")) c->prelaunch = atoi(e) != 0;
     c->num_cus = prop.multiProcessorCount;
     try {
       bind(c);
