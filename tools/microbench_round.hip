@@ -60,6 +60,36 @@ __global__ __launch_bounds__(kBlock) void k_round(const Fe* __restrict__ A, cons
   if (acc.v[0] == 0x12345u) out[0] = acc;  // keep the work alive
 }
 
+// round 0 body (k_gkr_round0: 2 threads per pair, 4 loads, 3 unreduced products)
+template <class F, int MODE>  // 0 real, 1 compute-only, 2 memory-only
+__global__ __launch_bounds__(kBlock) void k_round0(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                   const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t h,
+                                                   Fe* out) {
+  Wide w0 = wide_zero<F>(), w1 = wide_zero<F>(), w2 = wide_zero<F>();
+  uint64_t j, step;
+  uint32_t q;
+  pair_slot(j, q, step);
+  const Fe* __restrict__ X = q ? M : A;
+  const Fe* __restrict__ Z = q ? P : S;
+  const uint64_t mask = MODE == 1 ? (1u << 13) - 1 : ~0ull;
+  uint32_t x = 0;
+  for (; j < h; j += step) {
+    const uint64_t jj = j & mask, hh = MODE == 1 ? (1u << 13) : h;
+    const Fe x0 = ld_fe(X, jj), x1 = ld_fe(X, jj + hh), z0 = ld_fe(Z, jj), z1 = ld_fe(Z, jj + hh);
+    __builtin_amdgcn_sched_barrier(0);
+    if (MODE == 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x ^= x0.v[i] ^ x1.v[i] ^ z0.v[i] ^ z1.v[i];
+    } else {
+      wide_mac<F>(w0, x0, z0);
+      wide_mac<F>(w1, x1, z1);
+      wide_mac<F>(w2, at2<F>(x0, x1), at2<F>(z0, z1));
+    }
+  }
+  for (int i = 0; i < 17; ++i) x ^= w0.w[i] ^ w1.w[i] ^ w2.w[i];
+  if (x == 0x12345u) out[0].v[0] = x;  // keep the work alive
+}
+
 int main() {
   using F = Bn254Fr;
   const uint64_t N = 1ull << 24, h = N / 4;  // round 1 of a 24-var proof
@@ -91,6 +121,28 @@ int main() {
     printf("%-8s %8.1f us   %7.1f GB/s equivalent (grid %d = %d/CU)\n", name, us, bytes / (us * 1e-6) / 1e9, grid, per_cu);
     return 0;
   };
+  {
+    int pc0 = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc0, k_round0<F, 0>, kBlock, 0));
+    const int g0 = prop.multiProcessorCount * pc0;
+    const uint64_t h0 = N / 2;  // round 0 of a 24-var proof: 2^23 pairs over 4 tables of 2^24
+    auto run0 = [&](const char* name, auto kern) {
+      kern<<<g0, kBlock>>>(A, S, M, P, h0, out);
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 5; ++i) kern<<<g0, kBlock>>>(A, S, M, P, h0, out);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / 5, bytes = 256.0 * h0;
+      printf("round0 %-8s %8.1f us   %7.1f GB/s equivalent (grid %d = %d/CU)\n", name, us, bytes / (us * 1e-6) / 1e9, g0, pc0);
+      return 0;
+    };
+    run0("real", k_round0<F, 0>);
+    run0("compute", k_round0<F, 1>);
+    run0("memory", k_round0<F, 2>);
+  }
   run("real", k_round<F, 0>);
   run("compute", k_round<F, 1>);
   run("memory", k_round<F, 2>);
