@@ -141,6 +141,44 @@ int zk_gkr_sumcheck_verify(zk_field field, zk_repr repr, const zk_fe* coeffs /* 
                            zk_fe* out_challenges);
 
 /* ---------------------------------------------------------------------------
+ * Proof blob: a canonical byte form of a proof, so a proof
+ * produced on the CPU, on one GPU or on G GPUs can be compared as one digest
+ * and shipped/verified elsewhere. The reference keeps proofs as in-memory
+ * structs only (sum_check_protocol.rs:8-17); the blob holds exactly their
+ * fields. All integers little-endian; field elements canonical 32-byte LE
+ * (fq_vec_to_bytes, fiat_shamir_transcript.rs:32-37):
+ *   [0,4)   "ZKSP"
+ *   4       version = 1
+ *   5       kind: ZK_BLOB_GKR (gkr_prove) or ZK_BLOB_SUMCHECK (prove)
+ *   6       zk_field
+ *   7       0
+ *   [8,12)  nrounds (u32)
+ *   [12,44) claimed_sum
+ *   then per round: m (u8), m elements. For ZK_BLOB_GKR, m <= 3 is the trimmed
+ *   coefficient count and the m elements are exactly the bytes the transcript
+ *   absorbs that round; for ZK_BLOB_SUMCHECK they are the round's [s0, s1].
+ * Parsing rejects (ZK_EINVAL) a bad magic/version/kind/field, truncation,
+ * trailing bytes, m > 3 in a GKR blob, and elements >= p.
+ * Serialisers return the size in *out_len; pass out = NULL to query it.
+ * ------------------------------------------------------------------------- */
+enum { ZK_BLOB_GKR = 1, ZK_BLOB_SUMCHECK = 2 };
+int zk_gkr_proof_to_blob(zk_field field, zk_repr repr, const zk_fe* coeffs /* 3*nrounds */, const uint8_t* ncoeffs,
+                         uint32_t nrounds, const zk_fe* claimed_sum, uint8_t* out, size_t cap, size_t* out_len);
+int zk_sumcheck_proof_to_blob(zk_field field, zk_repr repr, const zk_fe* round_polys /* nrounds*poly_len */,
+                              uint32_t nrounds, uint32_t poly_len, const zk_fe* claimed_sum, uint8_t* out,
+                              size_t cap, size_t* out_len);
+int zk_proof_blob_info(const uint8_t* blob, size_t len, int* out_kind, zk_field* out_field, uint32_t* out_nrounds);
+int zk_gkr_proof_from_blob(const uint8_t* blob, size_t len, zk_repr repr, zk_fe* out_coeffs /* 3*cap_rounds */,
+                           uint8_t* out_ncoeffs /* cap_rounds */, uint32_t cap_rounds, zk_fe* out_claimed_sum);
+int zk_sumcheck_proof_from_blob(const uint8_t* blob, size_t len, zk_repr repr, zk_fe* out_round_polys,
+                                size_t cap_elems, uint32_t* out_poly_len, zk_fe* out_claimed_sum);
+/* gkr_verify of a GKR blob (claimed sum taken from the blob); outputs canonical. */
+int zk_gkr_verify_blob(const uint8_t* blob, size_t len, zk_transcript* transcript, int* out_verified,
+                       zk_fe* out_final_claimed_sum, zk_fe* out_challenges /* cap_rounds */, uint32_t cap_rounds);
+/* Keccak-256 (the transcript's sponge: rate 136, pad 0x01..0x80) of a byte string */
+int zk_keccak256(const uint8_t* data, size_t len, uint8_t out[32]);
+
+/* ---------------------------------------------------------------------------
  * Device-resident API (tables already in HBM, Montgomery form)
  * ------------------------------------------------------------------------- */
 int zk_dev_alloc(zk_ctx* ctx, size_t bytes, void** out);

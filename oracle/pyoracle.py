@@ -318,3 +318,22 @@ def synth(field: int, seed: int, table: int, index0: int, count: int) -> list[in
             v |= splitmix64((key + 4 * i + k) & M64) << (64 * k)
         out.append(v % p)
     return out
+
+
+# ---------------------------------------------------------------------------
+# Proof blob (format in include/zk_sumcheck.h "Proof blob"),
+# written independently of the library's serialiser so the tests compare two
+# implementations of the format. Test infrastructure only.
+# ---------------------------------------------------------------------------
+BLOB_GKR, BLOB_SUMCHECK = 1, 2
+
+
+def proof_blob(kind: int, field: int, claimed_sum: int, round_polys: list[list[int]]) -> bytes:
+    out = bytearray(b"ZKSP")
+    out += bytes([1, kind, field, 0])
+    out += len(round_polys).to_bytes(4, "little")
+    out += fq_vec_to_bytes([claimed_sum])
+    for poly in round_polys:
+        out += bytes([len(poly)])
+        out += fq_vec_to_bytes(list(poly))
+    return bytes(out)

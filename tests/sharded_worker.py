@@ -43,8 +43,11 @@ def main() -> None:
     tr = zk_amd.Transcript(field)
     check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, nloc, 0, ptr(as_limbs([0])), tr.h, ptr(coeffs),
                                                   ptr(nco), ptr(ch)))
-    res = {"polys": [[hex(x) for x in to_ints(coeffs[k, : nco[k]])] for k in range(n)],
-           "chal": [hex(x) for x in to_ints(ch[:n])], "collectives": ctx.stats()["collectives"]}
+    polys = [to_ints(coeffs[k, : nco[k]]) for k in range(n)]
+    blob = zk_amd.GkrProof([zk_amd.UnivariatePoly(p, field) for p in polys], 0, []).to_bytes(field)
+    res = {"polys": [[hex(x) for x in p] for p in polys],
+           "chal": [hex(x) for x in to_ints(ch[:n])], "collectives": ctx.stats()["collectives"],
+           "blob_keccak": zk_amd.keccak256(blob).hex()}
     with open(os.path.join(os.environ["OUT"], f"rank{rank}.json"), "w") as fh:
         json.dump(res, fh)
     dist.barrier()

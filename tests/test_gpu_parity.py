@@ -302,3 +302,17 @@ def test_stats_and_timing(ctx):
     assert k["gkr_round0"]["launches"] == 1 and k["gkr_round"]["launches"] == n - 1
     assert k["gkr_round"]["ms"] > 0 and st["host_syncs"] >= n
     assert k["gkr_round0"]["alg_bytes"] == 256 * (1 << (n - 1))
+
+
+@pytest.mark.parametrize("field", FIELDS)
+def test_gkr_proof_blob_digest_matches_oracle(ctx, field):
+    n = 16
+    tabs = [co.synth(field, 37, t, 0, 1 << n) for t in range(4)]
+    sp = SumPoly([ProductPoly([tabs[0], tabs[1]], field, ctx), ProductPoly([tabs[2], tabs[3]], field, ctx)])
+    claimed = sum(int(a) * int(s) + int(m) * int(q) for a, s, m, q in zip(*[to_ints(t) for t in tabs])) % zk_amd.modulus(field)
+    proof = zk_amd.gkr_prove(claimed, sp, Transcript(field), ctx)
+    blob = proof.to_bytes(field)
+    polys, chal = co.gkr_prove(field, tabs, co.Transcript())
+    assert zk_amd.keccak256(blob) == po.keccak256(po.proof_blob(po.BLOB_GKR, field, claimed, [list(p) for p in polys]))
+    v = zk_amd.gkr_verify_blob(blob, Transcript(field))
+    assert v.verified and v.random_challenges == list(chal)

@@ -18,6 +18,7 @@ import sys
 import pytest
 
 import coracle as co
+import pyoracle as po
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -54,7 +55,8 @@ def _run(world: int, comm: str, field: int, nloc: int, out: str, extra_env=None)
 def _oracle(field: int, n: int) -> dict:
     tabs = [co.synth(field, 19, t, 0, 1 << n) for t in range(4)]
     polys, chal = co.gkr_prove(field, tabs, co.Transcript())
-    return {"polys": [[hex(x) for x in p] for p in polys], "chal": [hex(x) for x in chal]}
+    return {"polys": [[hex(x) for x in p] for p in polys], "chal": [hex(x) for x in chal],
+            "blob_keccak": po.keccak256(po.proof_blob(po.BLOB_GKR, field, 0, [list(p) for p in polys])).hex()}
 
 
 @pytest.mark.parametrize("world,nloc,field", [(2, 12, 0), (4, 9, 2), (2, 0, 1)])
@@ -62,17 +64,21 @@ def test_host_comm_ranks_match_single_process(tmp_path, world, nloc, field):
     res = _run(world, "host", field, nloc, str(tmp_path))
     want = _oracle(field, nloc + world.bit_length() - 1)
     for rank, r in enumerate(res):
-        assert {"polys": r["polys"], "chal": r["chal"]} == want, f"rank {rank}"
+        assert {"polys": r["polys"], "chal": r["chal"]} == {"polys": want["polys"], "chal": want["chal"]}, f"rank {rank}"
+        # f4: the whole proof as one digest, identical on every rank and to the CPU oracle's
+        assert r["blob_keccak"] == want["blob_keccak"], f"rank {rank}"
         assert r["collectives"] == nloc + 1  # one all-reduce per local round + the tail gather
 
 
 def test_world1_without_comm(tmp_path):
     res = _run(1, "none", 0, 13, str(tmp_path))
-    assert {"polys": res[0]["polys"], "chal": res[0]["chal"]} == _oracle(0, 13)
+    want = _oracle(0, 13)
+    assert {"polys": res[0]["polys"], "chal": res[0]["chal"], "blob_keccak": res[0]["blob_keccak"]} == want
     assert res[0]["collectives"] == 0
 
 
 def test_rccl_data_path_forced_at_world1(tmp_path):
     res = _run(1, "rccl", 0, 14, str(tmp_path), {"ZK_FORCE_COLLECTIVES": "1"})
-    assert {"polys": res[0]["polys"], "chal": res[0]["chal"]} == _oracle(0, 14)
+    want = _oracle(0, 14)
+    assert {"polys": res[0]["polys"], "chal": res[0]["chal"], "blob_keccak": res[0]["blob_keccak"]} == want
     assert res[0]["collectives"] == 14  # every round went through ncclAllReduce

@@ -23,10 +23,13 @@ from .api import (  # noqa: F401
     SumPoly,
     Transcript,
     UnivariatePoly,
+    blob_info,
     default_context,
     fq_vec_to_bytes,
     gkr_prove,
     gkr_verify,
+    gkr_verify_blob,
+    keccak256,
     modulus,
     prove,
     verify,

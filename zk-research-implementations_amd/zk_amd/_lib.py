@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("ZK_LIB_PATH") or os.path.join(_HERE, "_lib", "libzksu
 PKG_ROOT = os.path.dirname(_HERE)
 
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
+ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
 KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth"]
 
@@ -63,6 +64,13 @@ SIGNATURES = {
     "zk_sumcheck_verify": (I, [P, I, I, P, U32, P, U32, U32, P, C.POINTER(C.c_int)]),
     "zk_gkr_sumcheck_prove": (I, [P, I, I, P, U32, P, P, P, P, P, P]),
     "zk_gkr_sumcheck_verify": (I, [I, I, P, P, U32, P, P, C.POINTER(C.c_int), P, P]),
+    "zk_gkr_proof_to_blob": (I, [I, I, P, P, U32, P, P, SZ, C.POINTER(SZ)]),
+    "zk_sumcheck_proof_to_blob": (I, [I, I, P, U32, U32, P, P, SZ, C.POINTER(SZ)]),
+    "zk_proof_blob_info": (I, [P, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(U32)]),
+    "zk_gkr_proof_from_blob": (I, [P, SZ, I, P, P, U32, P]),
+    "zk_sumcheck_proof_from_blob": (I, [P, SZ, I, P, SZ, C.POINTER(U32), P]),
+    "zk_gkr_verify_blob": (I, [P, SZ, P, C.POINTER(C.c_int), P, P, U32]),
+    "zk_keccak256": (I, [P, SZ, P]),
     "zk_dev_alloc": (I, [P, SZ, C.POINTER(C.c_void_p)]),
     "zk_dev_free": (I, [P, P]),
     "zk_dev_upload": (I, [P, I, I, P, SZ, P]),

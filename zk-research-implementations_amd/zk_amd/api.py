@@ -20,7 +20,7 @@ from enum import IntEnum
 
 import numpy as np
 
-from ._lib import ZK_EINVAL, ZkError, check, lib
+from ._lib import ZK_BLOB_GKR, ZK_BLOB_SUMCHECK, ZK_EINVAL, ZkError, check, lib
 from .context import REPR_CANONICAL, Context
 from .elems import as_limbs, one, ptr, to_ints
 
@@ -250,12 +250,93 @@ class Proof:  # :8-12
     proof_polynomials: list[list[int]]
     claimed_sum: int
 
+    def to_bytes(self, field: int = Field.BN254_FR) -> bytes:
+        """Canonical proof blob (include/zk_sumcheck.h "Proof blob", kind ZK_BLOB_SUMCHECK)."""
+        polys = self.proof_polynomials
+        plen = len(polys[0]) if polys else 2
+        if any(len(p) != plen for p in polys):
+            raise ValueError("round polynomials of different lengths")
+        flat = as_limbs([v for p in polys for v in p]) if polys and plen else np.zeros((1, 4), np.uint64)
+        return _blob(lambda out, cap, n: lib().zk_sumcheck_proof_to_blob(
+            int(field), REPR_CANONICAL, ptr(flat), len(polys), plen, ptr(one(self.claimed_sum)), out, cap, n))
+
+    @staticmethod
+    def from_bytes(blob: bytes) -> "Proof":
+        kind, _, n = blob_info(blob)
+        if kind != ZK_BLOB_SUMCHECK:
+            raise ValueError("ZK_EINVAL: not a sum-check proof blob")
+        cap = max(1, (len(blob) - 44) // 32)
+        rp = np.zeros((cap, 4), np.uint64)
+        plen = C.c_uint32(0)
+        cs = np.zeros((1, 4), np.uint64)
+        _call(lib().zk_sumcheck_proof_from_blob(blob, len(blob), REPR_CANONICAL, ptr(rp), cap, C.byref(plen), ptr(cs)))
+        vals = to_ints(rp[: n * plen.value])
+        m = plen.value
+        return Proof([vals[m * k: m * k + m] for k in range(n)], to_ints(cs)[0])
+
 
 @dataclass
 class GkrProof:  # :13-17
     proof_polynomials: list[UnivariatePoly]
     claimed_sum: int
     random_challenges: list[int]
+
+    def to_bytes(self, field: int | None = None) -> bytes:
+        """Canonical proof blob (kind ZK_BLOB_GKR): per round exactly the bytes the
+        transcript absorbs. The challenges are not stored (a verifier re-derives them)."""
+        if field is None:
+            field = self.proof_polynomials[0].field if self.proof_polynomials else Field.BN254_FR
+        coeffs, nco = _gkr_coeff_arrays(self.proof_polynomials)
+        return _blob(lambda out, cap, n: lib().zk_gkr_proof_to_blob(
+            int(field), REPR_CANONICAL, ptr(coeffs), ptr(nco), len(self.proof_polynomials),
+            ptr(one(self.claimed_sum)), out, cap, n))
+
+    @staticmethod
+    def from_bytes(blob: bytes) -> "GkrProof":
+        kind, field, n = blob_info(blob)
+        if kind != ZK_BLOB_GKR:
+            raise ValueError("ZK_EINVAL: not a GKR sum-check proof blob")
+        coeffs = np.zeros((max(n, 1), 3, 4), np.uint64)
+        nco = np.zeros(max(n, 1), np.uint8)
+        cs = np.zeros((1, 4), np.uint64)
+        _call(lib().zk_gkr_proof_from_blob(blob, len(blob), REPR_CANONICAL, ptr(coeffs), ptr(nco), max(n, 1), ptr(cs)))
+        polys = [UnivariatePoly(to_ints(coeffs[k, : nco[k]]), field) for k in range(n)]
+        return GkrProof(polys, to_ints(cs)[0], [])
+
+
+def _gkr_coeff_arrays(round_polys) -> tuple[np.ndarray, np.ndarray]:
+    n = len(round_polys)
+    coeffs = np.zeros((max(n, 1), 3, 4), np.uint64)
+    nco = np.zeros(max(n, 1), np.uint8)
+    for k, rp in enumerate(round_polys):
+        c = rp.coefficient if isinstance(rp, UnivariatePoly) else list(rp)
+        if len(c) > 3:
+            raise ValueError("round polynomial of degree > 2")
+        nco[k] = len(c)
+        if c:
+            coeffs[k, : len(c)] = as_limbs(c)
+    return coeffs, nco
+
+
+def _blob(fill) -> bytes:
+    n = C.c_size_t(0)
+    _call(fill(None, 0, C.byref(n)))
+    buf = (C.c_uint8 * n.value)()
+    _call(fill(buf, n.value, C.byref(n)))
+    return bytes(buf)
+
+
+def blob_info(blob: bytes) -> tuple[int, "Field", int]:
+    """(kind, field, nrounds) of a proof blob; raises ZkError on a malformed header."""
+    kind, field, n = C.c_int(0), C.c_int(0), C.c_uint32(0)
+    _call(lib().zk_proof_blob_info(blob, len(blob), C.byref(kind), C.byref(field), C.byref(n)))
+    return kind.value, Field(field.value), n.value
+
+
+def keccak256(data: bytes) -> bytes:
+    out = (C.c_uint8 * 32)()
+    _call(lib().zk_keccak256(data, len(data), out))
+    return bytes(out)
 
 
 @dataclass
@@ -310,20 +391,24 @@ def gkr_prove(claimed_sum: int, composed_polynomial: SumPoly, transcript: Transc
 def gkr_verify(round_polys: list[UnivariatePoly], claimed_sum: int, transcript: Transcript) -> GkrVerify:  # :117-150
     n = len(round_polys)
     field = transcript.field
-    coeffs = np.zeros((max(n, 1), 3, 4), np.uint64)
-    nco = np.zeros(max(n, 1), np.uint8)
-    for k, rp in enumerate(round_polys):
-        c = rp.coefficient if isinstance(rp, UnivariatePoly) else list(rp)
-        if len(c) > 3:
-            raise ValueError("round polynomial of degree > 2")
-        nco[k] = len(c)
-        if c:
-            coeffs[k, : len(c)] = as_limbs(c)
+    coeffs, nco = _gkr_coeff_arrays(round_polys)
     ok = C.c_int(0)
     fin = np.zeros((1, 4), np.uint64)
     ch = np.zeros((max(n, 1), 4), np.uint64)
     _call(lib().zk_gkr_sumcheck_verify(int(field), REPR_CANONICAL, ptr(coeffs), ptr(nco), n, ptr(one(claimed_sum)),
                                        transcript.h, C.byref(ok), ptr(fin), ptr(ch)))
+    if not ok.value:
+        return GkrVerify(False, 0, [0])
+    return GkrVerify(True, to_ints(fin)[0], to_ints(ch[:n]))
+
+
+def gkr_verify_blob(blob: bytes, transcript: Transcript) -> GkrVerify:
+    """gkr_verify of a GKR proof blob (claimed sum from the blob)."""
+    _, _, n = blob_info(blob)
+    ok = C.c_int(0)
+    fin = np.zeros((1, 4), np.uint64)
+    ch = np.zeros((max(n, 1), 4), np.uint64)
+    _call(lib().zk_gkr_verify_blob(blob, len(blob), transcript.h, C.byref(ok), ptr(fin), ptr(ch), max(n, 1)))
     if not ok.value:
         return GkrVerify(False, 0, [0])
     return GkrVerify(True, to_ints(fin)[0], to_ints(ch[:n]))
