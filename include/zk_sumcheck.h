@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 1u
+#define ZK_ABI_VERSION 2u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -75,7 +75,8 @@ enum {
   ZK_K_REDUCE = 4,     /* block partials -> limb-split sums */
   ZK_K_CONVERT = 5,    /* canonical <-> Montgomery */
   ZK_K_SYNTH = 6,      /* synthetic table generator */
-  ZK_K_KINDS = 7
+  ZK_K_LAYER = 7,      /* GKR circuit: layer evaluation, gate weights, layer tables */
+  ZK_K_KINDS = 8
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];
@@ -139,6 +140,39 @@ int zk_gkr_sumcheck_verify(zk_field field, zk_repr repr, const zk_fe* coeffs /* 
                            const uint8_t* ncoeffs, uint32_t nrounds, const zk_fe* claimed_sum,
                            zk_transcript* transcript, int* out_verified, zk_fe* out_final_claimed_sum,
                            zk_fe* out_challenges);
+
+/* ---------------------------------------------------------------------------
+ * GKR over a layered circuit (gkr_protocol.rs:31-227,
+ * gkr_circuit.rs:1-144). Layers are given input -> output: gates[l] gates in
+ * layer l, ops concatenated layer by layer (0 = Operation::Add, 1 = Mul), gate
+ * g of layer l reading (in[2g], in[2g+1]). Supported shape (the one for which
+ * the reference's table sizes agree; anything else is ZK_EINVAL): powers of
+ * two, ninputs = 2 gates[0], gates[l+1] = gates[l] / 2, output layer of 1 or
+ * 2 gates, 2 gates[0] <= 2^14.
+ * The prover evaluates the circuit, builds every layer's four sum-check tables
+ * (wiring folded at the verifier's points — sparse, instead of the reference's
+ * dense 2^(3g+2) add_i / mul_i — and the tensor sum / product of w) and runs
+ * the layer sum-checks on the GPU; the transcript is the reference's (fresh,
+ * output poly absorbed first, alpha / beta per layer). The input layer's KZG
+ * commitment (:92-118, row f3) is not made: the two input-MLE evaluations it
+ * would open are returned instead, and the verifier recomputes them when
+ * given the inputs.
+ * Outputs (rounds in processing order: output layer first; layer l has
+ * 2 log2(2 gates[l]) rounds, total from zk_gkr_circuit_rounds):
+ *   out_output_poly[2], out_coeffs[3*total] + out_ncoeffs[total] (trimmed),
+ *   out_challenges[total], out_claims[2*(nlayers-1)] = (o1, o2) per layer
+ *   except the input layer, out_input_evals[2].
+ * ------------------------------------------------------------------------- */
+int zk_gkr_circuit_rounds(uint32_t nlayers, const uint32_t* gates, uint32_t* out_total_rounds);
+int zk_gkr_circuit_prove(zk_ctx* ctx, zk_field field, zk_repr repr, uint32_t nlayers, const uint32_t* gates,
+                         const uint8_t* ops, const zk_fe* inputs, uint32_t ninputs, zk_fe* out_output_poly,
+                         zk_fe* out_coeffs, uint8_t* out_ncoeffs, zk_fe* out_challenges, zk_fe* out_claims,
+                         zk_fe* out_input_evals);
+/* gkr::verify (host). inputs may be NULL (then the input evaluations are not
+ * re-derived, matching a verifier that trusts the commitment opening). */
+int zk_gkr_circuit_verify(zk_field field, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                          const zk_fe* inputs, uint32_t ninputs, const zk_fe* output_poly, const zk_fe* coeffs,
+                          const uint8_t* ncoeffs, const zk_fe* claims, const zk_fe* input_evals, int* out_verified);
 
 /* ---------------------------------------------------------------------------
  * Proof blob: a canonical byte form of a proof, so a proof

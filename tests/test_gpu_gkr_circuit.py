@@ -1,0 +1,67 @@
+"""GKR over a layered circuit on the GPU: circuit evaluation,
+sparse-wiring layer tables and layer sum-checks on the device, through the C
+ABI. Small circuits must equal the dense reference restatement
+(oracle/gkr_oracle.py) exactly; a 2^10-input circuit (input-layer sum-check
+over 20 variables) must pass the verifier (size-independent property)."""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+import gkr_oracle as go
+
+from zk_amd.gkr import Circuit, Operation, prove, verify
+
+pytestmark = pytest.mark.gpu
+A, M = go.ADD, go.MUL
+OPS = {A: Operation.Add, M: Operation.Mul}
+
+
+def _circuit(rng: random.Random, depth: int, out_gates: int) -> list[list[str]]:
+    return [[rng.choice((A, M)) for _ in range(out_gates << (depth - 1 - i))] for i in range(depth)]
+
+
+@pytest.mark.parametrize("field,depth,out_gates", [(2, 3, 1), (0, 3, 1), (1, 4, 2), (2, 5, 1), (0, 1, 1), (0, 1, 2),
+                                                   (2, 2, 2), (0, 5, 2)])
+def test_device_proof_equals_oracle(ctx, field, depth, out_gates):
+    rng = random.Random(1000 * field + 10 * depth + out_gates)
+    structure = _circuit(rng, depth, out_gates)
+    p = go.MODULI[field]
+    inputs = [rng.randrange(p) for _ in range(2 * len(structure[0]))]
+    want = go.prove(field, structure, inputs)
+    circ = Circuit([[OPS[o] for o in layer] for layer in structure], field)
+    got = prove(circ, inputs, ctx)
+    assert got.output_poly == want["output_poly"]
+    assert [[q.coefficient for q in layer] for layer in got.proof_polynomials] == \
+        [[list(q) for q in layer] for layer in want["proof_polynomials"]]
+    assert got.claimed_evaluations == [tuple(c) for c in want["claimed_evaluations"]]
+    assert got.input_evaluations == tuple(want["input_evaluations"])
+    assert verify(got, circ, inputs)
+
+
+def test_reference_circuit(ctx):  # gkr_protocol.rs:473-506
+    structure = [[A, A, A, A], [M, A], [A]]
+    inputs = [5, 2, 2, 4, 10, 0, 3, 3]
+    circ = Circuit([[OPS[o] for o in layer] for layer in structure], 2)
+    got = prove(circ, inputs, ctx)
+    want = go.prove(2, structure, inputs)
+    assert got.output_poly == want["output_poly"] == [58, 0]  # (5+2)(2+4) + (10+0)+(3+3)
+    assert verify(got, circ, inputs)
+
+
+@pytest.mark.parametrize("field", [0, 2])
+def test_large_circuit_verifies(ctx, field):
+    rng = random.Random(77 + field)
+    depth = 10  # 1024 inputs; input layer: 512 gates, tables of 2^20, 20 rounds
+    structure = [[rng.choice((Operation.Add, Operation.Mul)) for _ in range(1 << (depth - 1 - i))] for i in range(depth)]
+    p = go.MODULI[field]
+    inputs = [rng.randrange(p) for _ in range(1 << depth)]
+    circ = Circuit(structure, field)
+    proof = prove(circ, inputs, ctx)
+    assert proof.output_poly[0] == circ.evaluate(inputs)[-1][0] and proof.output_poly[1] == 0
+    assert [len(layer) for layer in proof.proof_polynomials] == [2 * (i + 1) for i in range(depth)]
+    assert verify(proof, circ, inputs)
+    bad = list(inputs)
+    bad[123] = (bad[123] + 1) % p
+    assert not verify(proof, circ, bad)

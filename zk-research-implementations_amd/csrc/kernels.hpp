@@ -626,4 +626,72 @@ __global__ __launch_bounds__(kBlock) void k_synth(Fe* Y, uint64_t n, uint64_t ke
   }
 }
 
+// ---------------------------------------------------------------------------
+// GKR layer tables on device. A layer of G gates reads L = 2G
+// values w (its inputs). The reference builds the wiring predicate add_i /
+// mul_i densely over 2^(3g+2) points (gkr_circuit.rs:39-104) and folds its
+// output bits (partial_evaluate / multi_partial_evaluate, scale, add:
+// gkr_protocol.rs:243-292); the folded table over (b, c) in [0, L)^2 is
+// nonzero only at (2 idx, 2 idx + 1), where it equals
+//   weight(idx) = alpha * eq(r_b, idx) + beta * eq(r_c, idx)
+// for a gate of that op (eq over the idx field, MSB first; the output layer
+// folds one variable with r0: alpha = 1, no beta term). So one streaming pass
+// writes all four sum-check tables: A (add wiring), S = w_b + w_c, M (mul
+// wiring), P = w_b * w_c at t = i L + j (tensor_add_mul_polynomials order).
+// ---------------------------------------------------------------------------
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_gate_weights(const Fe* __restrict__ rb, const Fe* __restrict__ rc,
+                                                         uint32_t W, Fe alpha, Fe beta, uint32_t has_c, uint32_t G,
+                                                         Fe* __restrict__ out) {
+  const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
+  if (idx >= G) return;
+  const Fe one = fe_one<F>();
+  Fe eb = one, ec = one;
+  for (uint32_t k = 0; k < W; ++k) {
+    const bool bit = (idx >> (W - 1 - k)) & 1u;
+    const Fe xb = ld_fe(rb, k);
+    eb = fe_mul<F>(eb, bit ? xb : fe_sub<F>(one, xb));
+    if (has_c) {
+      const Fe xc = ld_fe(rc, k);
+      ec = fe_mul<F>(ec, bit ? xc : fe_sub<F>(one, xc));
+    }
+  }
+  Fe wgt = fe_mul<F>(alpha, eb);
+  if (has_c) wgt = fe_add<F>(wgt, fe_mul<F>(beta, ec));
+  st_fe(out, idx, wgt);
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_layer_tables(const Fe* __restrict__ w, uint32_t lgL,
+                                                         const Fe* __restrict__ wt, const uint8_t* __restrict__ ops,
+                                                         Fe* __restrict__ A, Fe* __restrict__ S, Fe* __restrict__ M,
+                                                         Fe* __restrict__ P) {
+  const uint64_t T = (uint64_t)1 << (2 * lgL), Lm = ((uint64_t)1 << lgL) - 1;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < T; t += stride) {
+    const uint64_t i = t >> lgL, j = t & Lm;
+    const Fe wi = ld_fe(w, i), wj = ld_fe(w, j);
+    Fe a = fe_zero<F>(), m = fe_zero<F>();
+    if ((i & 1) == 0 && j == i + 1) {
+      const Fe x = ld_fe(wt, i >> 1);
+      if (ops[i >> 1]) m = x;
+      else a = x;
+    }
+    st_fe(A, t, a);
+    st_fe(S, t, fe_add<F>(wi, wj));
+    st_fe(M, t, m);
+    st_fe(P, t, fe_mul<F>(wi, wj));
+  }
+}
+
+// one circuit layer (gkr_circuit.rs:127-143): out[g] = in[2g] op in[2g+1]
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_circuit_layer(const Fe* __restrict__ in, const uint8_t* __restrict__ ops,
+                                                          uint32_t G, Fe* __restrict__ out) {
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= G) return;
+  const Fe a = ld_fe(in, 2 * (uint64_t)g), b = ld_fe(in, 2 * (uint64_t)g + 1);
+  st_fe(out, g, ops[g] ? fe_mul<F>(a, b) : fe_add<F>(a, b));
+}
+
 }  // namespace zk

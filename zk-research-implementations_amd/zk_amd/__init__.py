@@ -35,4 +35,5 @@ from .api import (  # noqa: F401
     verify,
 )
 from .context import Context, DeviceTable  # noqa: F401
+from . import gkr  # noqa: F401  (gkr crate mirror: Circuit, Operation, prove, verify)
 from ._lib import ZkError  # noqa: F401

@@ -17,7 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth"]
+KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer"]
 
 
 class ZkError(RuntimeError):
@@ -28,10 +28,10 @@ class ZkError(RuntimeError):
 
 class ZkStats(C.Structure):
     _fields_ = [
-        ("launches", C.c_uint64 * 7),
-        ("kernel_ms", C.c_double * 7),
-        ("alg_bytes", C.c_double * 7),
-        ("field_muls", C.c_double * 7),
+        ("launches", C.c_uint64 * 8),
+        ("kernel_ms", C.c_double * 8),
+        ("alg_bytes", C.c_double * 8),
+        ("field_muls", C.c_double * 8),
         ("host_syncs", C.c_uint64),
         ("collectives", C.c_uint64),
         ("host_wait_us", C.c_double),
@@ -64,6 +64,9 @@ SIGNATURES = {
     "zk_sumcheck_verify": (I, [P, I, I, P, U32, P, U32, U32, P, C.POINTER(C.c_int)]),
     "zk_gkr_sumcheck_prove": (I, [P, I, I, P, U32, P, P, P, P, P, P]),
     "zk_gkr_sumcheck_verify": (I, [I, I, P, P, U32, P, P, C.POINTER(C.c_int), P, P]),
+    "zk_gkr_circuit_rounds": (I, [U32, P, C.POINTER(U32)]),
+    "zk_gkr_circuit_prove": (I, [P, I, I, U32, P, P, P, U32, P, P, P, P, P, P]),
+    "zk_gkr_circuit_verify": (I, [I, I, U32, P, P, P, U32, P, P, P, P, P, C.POINTER(C.c_int)]),
     "zk_gkr_proof_to_blob": (I, [I, I, P, P, U32, P, P, SZ, C.POINTER(SZ)]),
     "zk_sumcheck_proof_to_blob": (I, [I, I, P, U32, U32, P, P, SZ, C.POINTER(SZ)]),
     "zk_proof_blob_info": (I, [P, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(U32)]),

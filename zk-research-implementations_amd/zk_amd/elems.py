@@ -39,4 +39,6 @@ def one(v: int) -> np.ndarray:
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:
-    return C.c_void_p(a.ctypes.data)
+    """Pointer to a's data that keeps a alive (numpy's data_as holds a reference),
+    so `f(ptr(as_limbs(x)))` cannot hand the C side a freed temporary."""
+    return a.ctypes.data_as(C.c_void_p)
