@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--cpu-sample-nvars", type=int, default=22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true")
+    ap.add_argument("--no-circuit", action="store_true", help="skip the full GKR circuit prove (SURVEY 8(f2))")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
     return ap.parse_args()
 
@@ -107,6 +108,45 @@ def fold_bench(ctx, field: int, nvars: int = 20, reps: int = 10) -> dict:
         "bytes_per_launch": k["alg_bytes"] / k["launches"],
         "achieved_GBs": gbs,
         "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
+    }
+
+
+def circuit_bench(ctx, field: int, log_inputs: int = 12, reps: int = 3) -> dict:
+    """a full GKR prove over a random binary-tree circuit with
+    2^log_inputs inputs — circuit evaluation, every layer's four tables (sparse
+    wiring) and sum-checks on the device, transcript on the host. The input
+    layer's sum-check runs over 2*log_inputs variables (24 at the default)."""
+    import random
+
+    import zk_amd
+    from zk_amd.gkr import Circuit, Operation, prove, verify
+
+    rng = random.Random(11)
+    structure = [[rng.choice((Operation.Add, Operation.Mul)) for _ in range(1 << (log_inputs - 1 - i))]
+                 for i in range(log_inputs)]
+    p = zk_amd.modulus(field)
+    inputs = [rng.randrange(p) for _ in range(1 << log_inputs)]
+    circ = Circuit(structure, field)
+    proof = prove(circ, inputs, ctx)  # warm-up
+    ok = verify(proof, circ, inputs)
+    ctx.reset_stats()
+    ctx.set_timing_kinds(["layer"])
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        prove(circ, inputs, ctx)
+        times.append(time.perf_counter() - t0)
+    ctx.set_timing(False)
+    k = ctx.stats()["kernels"]["layer"]
+    times.sort()
+    return {
+        "workload": f"gkr::prove over a random {log_inputs}-layer binary-tree circuit, {1 << log_inputs} inputs "
+                    f"(input-layer sum-check over {2 * log_inputs} variables), {'BN254 Fr' if field == 0 else field}",
+        "ms_median": times[len(times) // 2] * 1e3,
+        "verified": ok,
+        "layer_kernels_ms_per_proof": k["ms"] / reps,
+        "layer_tables_GBs": k["alg_bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] else None,
+        "note": "the reference builds add_i/mul_i densely (2^(3g+2) entries: 2^35 at this size) and cannot run it",
     }
 
 
@@ -255,6 +295,8 @@ def main() -> None:
         }
         if not args.no_fold:
             out["fold_20var"] = fold_bench(ctx, field)
+        if not args.no_circuit and world == 1:
+            out["gkr_circuit"] = circuit_bench(ctx, field)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(field, args.cpu_sample_nvars)
             out["cpu_baseline"] = cb
