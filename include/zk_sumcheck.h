@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 2u
+#define ZK_ABI_VERSION 3u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -76,7 +76,8 @@ enum {
   ZK_K_CONVERT = 5,    /* canonical <-> Montgomery */
   ZK_K_SYNTH = 6,      /* synthetic table generator */
   ZK_K_LAYER = 7,      /* GKR circuit: layer evaluation, gate weights, layer tables */
-  ZK_K_KINDS = 8
+  ZK_K_MSM = 8,        /* KZG: bucket sort, bucket/window sums, fixed-base setup, normalisation */
+  ZK_K_KINDS = 9
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];
@@ -173,6 +174,35 @@ int zk_gkr_circuit_prove(zk_ctx* ctx, zk_field field, zk_repr repr, uint32_t nla
 int zk_gkr_circuit_verify(zk_field field, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
                           const zk_fe* inputs, uint32_t ninputs, const zk_fe* output_poly, const zk_fe* coeffs,
                           const uint8_t* ncoeffs, const zk_fe* claims, const zk_fe* input_evals, int* out_verified);
+
+/* ---------------------------------------------------------------------------
+ * Multilinear KZG over BLS12-381 G1 (pcs/src/kzg_pcs/kzg.rs).
+ * Scalars are BLS12-381 Fr (zk_fe, repr as elsewhere). Points are affine with
+ * canonical little-endian 48-byte coordinates; (0, 0) is the point at infinity.
+ *   zk_kzg_setup       KZG::new / run_trusted_setup's G1 half (:18-49): the
+ *                      Lagrange basis eq(taus, i) * G for every i (MSB-first
+ *                      hypercube, generate_bhc :171-181), plus the bases over
+ *                      every suffix of taus used by get_proof. The G2 taus
+ *                      (for the pairing-based KZG::verify) are not built.
+ *   zk_kzg_commit      KZG::commit (:51-53) = sum_i evals[i] * L_i (Pippenger MSM)
+ *   zk_kzg_get_proof   KZG::get_proof (:59-95): nvars quotient commitments
+ *   zk_kzg_lagrange_basis  the basis over the last nvars_suffix taus
+ *   zk_msm_g1          sum_i scalars[i] * bases[i] for caller bases (checked on the curve)
+ * KZG::open is MultilinearPoly::evaluate: zk_mle_evaluate.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  uint64_t x[6];
+  uint64_t y[6];
+} zk_g1;
+typedef struct zk_kzg zk_kzg;
+int zk_kzg_setup(zk_ctx* ctx, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_kzg** out);
+void zk_kzg_free(zk_kzg* kzg);
+int zk_kzg_lagrange_basis(zk_ctx* ctx, const zk_kzg* kzg, uint32_t nvars_suffix, zk_g1* out /* 2^nvars_suffix */);
+int zk_kzg_commit(zk_ctx* ctx, const zk_kzg* kzg, zk_repr repr, const zk_fe* evals /* 2^nvars */, zk_g1* out);
+int zk_dev_kzg_commit(zk_ctx* ctx, const zk_kzg* kzg, const void* dev_evals /* Montgomery Fr */, zk_g1* out);
+int zk_kzg_get_proof(zk_ctx* ctx, const zk_kzg* kzg, zk_repr repr, const zk_fe* evals, const zk_fe* opened_value,
+                     const zk_fe* point /* nvars */, zk_g1* out /* nvars */);
+int zk_msm_g1(zk_ctx* ctx, zk_repr repr, const zk_g1* bases, const zk_fe* scalars, size_t n, zk_g1* out);
 
 /* ---------------------------------------------------------------------------
  * Proof blob: a canonical byte form of a proof, so a proof

@@ -1,0 +1,129 @@
+"""Multilinear KZG over BLS12-381 G1 on the GPU, through the
+C ABI, against the reference-faithful restatement (oracle/kzg_oracle.py) and
+the reference's own KZG tests (pcs/src/kzg_pcs/kzg.rs:214-464). With known
+taus every commitment is also checked against f(taus) * G (the MLE value
+times the generator: sum_i f_i eq(taus, i) = f(taus)), a size-independent
+property that pins large MSMs with one scalar multiplication."""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+import kzg_oracle as ko
+import pyoracle as po
+
+from zk_amd.kzg import KZG, msm_g1
+
+pytestmark = pytest.mark.gpu
+R = ko.R
+TAUS = [5, 2, 3]
+EVALS = [0, 4, 0, 4, 0, 4, 3, 7]
+
+
+def test_reference_kzg_tests(ctx):  # kzg.rs:233-400
+    k = KZG(TAUS, ctx)
+    want = [(-8) % R, 12, 16, (-24) % R, 10, (-15) % R, (-20) % R, 30]
+    assert k.lagrange_basis() == [ko.mul(x, ko.G1) for x in want]
+    assert k.commit(EVALS) == ko.mul(42, ko.G1)
+    point = [6, 4, 0]
+    v = k.open(point, EVALS)
+    assert v == 72
+    assert k.get_proof(v, point, EVALS) == [ko.mul(x, ko.G1) for x in (6, 18, 4)]
+    k.close()
+
+
+def test_suffix_bases(ctx):
+    rng = random.Random(3)
+    taus = [rng.randrange(R) for _ in range(5)]
+    k = KZG(taus, ctx)
+    for v in range(0, 6):
+        assert k.lagrange_basis(v) == ko.get_lagrange_basis(taus[5 - v:]) if v else [ko.G1]
+    k.close()
+
+
+@pytest.mark.parametrize("n", [1, 6])
+def test_commit_equals_naive_oracle(ctx, n):
+    rng = random.Random(10 + n)
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    k = KZG(taus, ctx)
+    c = k.commit(evals)
+    assert c == ko.commit(evals, ko.get_lagrange_basis(taus))
+    assert c == ko.mul(po.evaluate(R, evals, taus), ko.G1)
+    k.close()
+
+
+def test_large_commit_equals_mle_value_times_g(ctx):
+    rng = random.Random(99)
+    n = 14
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    k = KZG(taus, ctx)
+    assert k.commit(evals) == ko.mul(po.evaluate(R, evals, taus), ko.G1)
+    k.close()
+
+
+def test_skewed_scalars(ctx):
+    rng = random.Random(5)
+    n = 12
+    taus = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    N = 1 << n
+    assert k.commit([7] * N) == ko.mul(7, ko.G1)  # sum_i L_i = G
+    assert k.commit([0] * N) is None
+    one_hot = [0] * N
+    one_hot[1234] = rng.randrange(R)
+    assert k.commit(one_hot) == ko.mul(one_hot[1234] * po.evaluate(R, [int(i == 1234) for i in range(N)], taus), ko.G1)
+    small = [rng.randrange(16) for _ in range(N)]
+    assert k.commit(small) == ko.mul(po.evaluate(R, small, taus), ko.G1)
+    assert k.commit([R - 1] * N) == ko.neg(ko.G1)
+    k.close()
+
+
+def test_get_proof_matches_reference_faithful_oracle(ctx):
+    rng = random.Random(8)
+    n = 5
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    point = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    v = k.open(point, evals)
+    assert v == po.evaluate(R, evals, point)
+    assert k.get_proof(v, point, evals) == ko.get_proof(evals, v, point, ko.get_lagrange_basis(taus))
+    k.close()
+
+
+def test_get_proof_quotients_at_taus(ctx):
+    rng = random.Random(9)
+    n = 12
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    point = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    v = k.open(point, evals)
+    proof = k.get_proof(v, point, evals)
+    cur = [(e - v) % R for e in evals]
+    for i in range(n):
+        q = ko.get_quotient(cur)
+        assert proof[i] == ko.mul(po.evaluate(R, q, taus[i + 1:]) if len(q) > 1 else q[0], ko.G1), i
+        cur = ko.get_remainder(cur, point[i])
+    k.close()
+
+
+def test_msm_arbitrary_bases(ctx):
+    rng = random.Random(12)
+    bases = [ko.mul(rng.randrange(R), ko.G1) for _ in range(100)] + [None]
+    scalars = [rng.randrange(R) for _ in range(len(bases))]
+    want = None
+    for s, b in zip(scalars, bases):
+        want = ko.add(want, ko.mul(s, b))
+    assert msm_g1(bases, scalars, ctx) == want
+    assert msm_g1([], [], ctx) is None
+
+
+def test_invalid_inputs(ctx):
+    with pytest.raises(ValueError, match="not on the curve"):
+        msm_g1([(1, 2)], [1], ctx)
+    with pytest.raises(ValueError, match="Invalid num of vars"):
+        KZG([], ctx)

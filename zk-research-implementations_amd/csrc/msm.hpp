@@ -1,0 +1,235 @@
+// gfx950 kernels of the multilinear KZG commitment over BLS12-381 G1
+// (pcs/src/kzg_pcs/kzg.rs). Host orchestration in
+// zk_sumcheck.hip ("KZG").
+//
+// MSM (Pippenger). The reference commits with a naive sum of n full scalar
+// multiplications (evaluate_poly_with_l_basis_in_g1, kzg.rs:131-144). Here:
+// scalars are cut into W = ceil(255 / c) windows of c bits; every nonzero
+// digit puts its point into bucket (w, d) (counting sort: histogram, scan,
+// scatter); buckets are summed by a segmented reduction (tasks of <= kSegTask
+// points, repeated over the partial sums until every bucket is one task, so a
+// skewed scalar distribution — all equal, all zero — never serialises on one
+// thread); each window's sum_d d * B_d comes from running sums over chunks of
+// buckets; the host combines the W window sums (Horner, c doublings each).
+// Every step is exact group arithmetic, so the result is the same group
+// element as the reference's.
+#pragma once
+#include "ec.hpp"
+#include "kernels.hpp"
+
+namespace zk {
+
+constexpr uint32_t kSegTask = 32;    // points summed by one thread per reduction level
+constexpr uint32_t kBucketChunk = 32;  // buckets per thread in the window reduction
+
+__device__ __forceinline__ Fq ld_fq(const Fq* p, uint64_t i) { return p[i]; }
+
+// ---- exclusive scan of u32 (in place), 2048 per block ------------------------
+constexpr uint32_t kScanPer = 8, kScanBlock = kBlock * kScanPer;
+__global__ __launch_bounds__(kBlock) void k_scan_block(uint32_t* __restrict__ a, uint64_t n,
+                                                       uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t s[kBlock];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlock + (uint64_t)threadIdx.x * kScanPer;
+  uint32_t v[kScanPer], tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    v[k] = base + k < n ? a[base + k] : 0u;
+    tot += v[k];
+  }
+  s[threadIdx.x] = tot;
+  __syncthreads();
+  for (uint32_t off = 1; off < kBlock; off <<= 1) {  // Hillis-Steele inclusive scan of the thread totals
+    const uint32_t x = threadIdx.x >= off ? s[threadIdx.x - off] : 0u;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint32_t run = s[threadIdx.x] - tot;  // exclusive prefix of this thread
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    if (base + k < n) a[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == kBlock - 1 && block_sums) block_sums[blockIdx.x] = s[kBlock - 1];
+}
+__global__ __launch_bounds__(kBlock) void k_scan_add(uint32_t* __restrict__ a, uint64_t n,
+                                                     const uint32_t* __restrict__ block_off) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) a[i] += block_off[i / kScanBlock];
+}
+
+// ---- bucket sort --------------------------------------------------------------
+// digit w of a canonical 255-bit scalar (8 x u32 LE)
+__device__ __forceinline__ uint32_t scalar_digit(const Fe& s, uint32_t bit, uint32_t c) {
+  const uint32_t wi = bit >> 5, sh = bit & 31;
+  uint64_t x = s.v[wi];
+  if (wi + 1 < 8) x |= (uint64_t)s.v[wi + 1] << 32;
+  return (uint32_t)(x >> sh) & ((1u << c) - 1u);
+}
+// counts[w * 2^c + d] += 1 for every point with digit d != 0 in window w
+__global__ __launch_bounds__(kBlock) void k_msm_count(const Fe* __restrict__ scalars, uint64_t n, uint32_t c, uint32_t W,
+                                                      uint32_t* __restrict__ counts) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const Fe s = ld_fe(scalars, i);
+    for (uint32_t w = 0; w < W; ++w) {
+      const uint32_t d = scalar_digit(s, w * c, c);
+      if (d) atomicAdd(counts + ((uint64_t)w << c) + d, 1u);
+    }
+  }
+}
+// order[cursor[key]++] = i (cursor = exclusive scan of counts)
+__global__ __launch_bounds__(kBlock) void k_msm_scatter(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
+                                                        uint32_t W, uint32_t* __restrict__ cursor,
+                                                        uint32_t* __restrict__ order) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const Fe s = ld_fe(scalars, i);
+    for (uint32_t w = 0; w < W; ++w) {
+      const uint32_t d = scalar_digit(s, w * c, c);
+      if (d) order[atomicAdd(cursor + ((uint64_t)w << c) + d, 1u)] = (uint32_t)i;
+    }
+  }
+}
+
+// ---- segmented reduction --------------------------------------------------------
+// Segment s = items [off[s], off[s+1]). Level: segment s gets ceil(len/T) tasks
+// (at least 1, so empty segments yield infinity); task t of segment s sums
+// items [off[s] + k T, min(off[s+1], off[s] + (k+1) T)).
+__global__ __launch_bounds__(kBlock) void k_seg_task_counts(const uint32_t* __restrict__ off, uint64_t nseg,
+                                                            uint32_t* __restrict__ tasks) {
+  const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (s >= nseg) return;
+  const uint32_t len = off[s + 1] - off[s];
+  tasks[s] = len ? (len + kSegTask - 1) / kSegTask : 1u;
+}
+// task_seg[task_off[s] + k] = s
+__global__ __launch_bounds__(kBlock) void k_seg_task_owner(const uint32_t* __restrict__ task_off, uint64_t nseg,
+                                                           uint32_t ntasks, uint32_t* __restrict__ task_seg) {
+  const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (s >= nseg) return;
+  const uint32_t a = task_off[s], b = s + 1 < nseg ? task_off[s + 1] : ntasks;
+  for (uint32_t t = a; t < b; ++t) task_seg[t] = (uint32_t)s;
+}
+// GATHER: items are affine bases[order[j]]; else contiguous Jacobian points
+template <bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ bases, const uint32_t* __restrict__ order,
+                                                    const G1J* __restrict__ items, const uint32_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ task_off,
+                                                    const uint32_t* __restrict__ task_seg, uint32_t ntasks,
+                                                    G1J* __restrict__ out) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= ntasks) return;
+  const uint32_t s = task_seg[t], k = t - task_off[s];
+  const uint32_t a = off[s] + k * kSegTask, e = off[s + 1];
+  const uint32_t b = a + kSegTask < e ? a + kSegTask : e;
+  G1J acc = g1_inf();
+  for (uint32_t j = a; j < b; ++j) {
+    if (GATHER) acc = g1_add_mixed(acc, bases[order[j]]);
+    else acc = g1_add(acc, items[j]);
+  }
+  out[t] = acc;
+}
+
+// ---- window reduction -----------------------------------------------------------
+// For window w, chunk j of buckets d in [lo, hi): sum_d d B_d = u + lo * T with
+// T = sum B_d, u = sum (d - lo) B_d (running sum from the top).
+__global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict__ buckets, uint32_t c, uint32_t W,
+                                                          G1J* __restrict__ out) {
+  const uint32_t chunks = (1u << c) / kBucketChunk;
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= W * chunks) return;
+  const uint32_t w = g / chunks, lo = (g % chunks) * kBucketChunk, hi = lo + kBucketChunk;
+  const G1J* B = buckets + ((uint64_t)w << c);
+  G1J t = g1_inf(), u = g1_inf();
+  for (uint32_t d = hi; d-- > lo;) {
+    t = g1_add(t, B[d]);
+    if (d > lo) u = g1_add(u, t);
+  }
+  out[g] = lo ? g1_add(u, g1_mul_small(t, lo)) : u;  // d = 0 (lo = 0) has weight 0: u already is sum d B_d
+}
+
+// ---- fixed-base scalar multiplication (Lagrange basis setup) ----------------------
+// table[w * 256 + d] = d * 2^(8w) * G (affine); out[i] = scalars[i] * G
+__global__ __launch_bounds__(kBlock) void k_fixed_base(const G1A* __restrict__ table, const Fe* __restrict__ scalars,
+                                                       uint64_t n, G1J* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const Fe s = ld_fe(scalars, i);
+    G1J acc = g1_inf();
+    for (uint32_t w = 0; w < 32; ++w) {
+      const uint32_t d = (s.v[w >> 2] >> ((w & 3) * 8)) & 0xffu;
+      if (d) acc = g1_add_mixed(acc, table[w * 256 + d]);
+    }
+    out[i] = acc;
+  }
+}
+
+// eq(taus, i) over n variables, MSB first (get_lagrange_basis's scalars, kzg.rs:183-206); canonical out
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_eq_scalars(const Fe* __restrict__ taus, uint32_t nv, uint64_t count,
+                                                       Fe* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const Fe one = fe_one<F>();
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride) {
+    Fe e = one;
+    for (uint32_t k = 0; k < nv; ++k) {
+      const Fe tk = ld_fe(taus, k);
+      e = fe_mul<F>(e, ((i >> (nv - 1 - k)) & 1) ? tk : fe_sub<F>(one, tk));
+    }
+    st_fe(out, i, fe_from_mont<F>(e));
+  }
+}
+
+// Jacobian -> affine, kBatchNorm points per thread sharing one inversion
+// (Montgomery's trick); the prefix products are parked in out[].x until the
+// backward pass overwrites them; infinity stays (0, 0)
+constexpr uint32_t kBatchNorm = 32;
+__global__ __launch_bounds__(kBlock) void k_batch_normalize(const G1J* __restrict__ in, uint64_t n,
+                                                            G1A* __restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t a = t * kBatchNorm;
+  if (a >= n) return;
+  const uint32_t m = (uint32_t)(n - a < kBatchNorm ? n - a : kBatchNorm);
+  Fq acc = fq_one();
+  for (uint32_t k = 0; k < m; ++k) {
+    out[a + k].x = acc;  // product of the nonzero Z's before k
+    const Fq z = in[a + k].Z;
+    if (!fq_is_zero(z)) acc = fq_mul(acc, z);
+  }
+  Fq inv = fq_inv(acc);  // (prod Z)^-1
+  for (uint32_t k = m; k-- > 0;) {
+    const G1J p = in[a + k];
+    if (fq_is_zero(p.Z)) {
+      out[a + k] = {fq_zero(), fq_zero()};
+      continue;
+    }
+    const Fq zi = fq_mul(inv, out[a + k].x);
+    inv = fq_mul(inv, p.Z);
+    out[a + k] = g1_to_affine_zi(p, zi);
+  }
+}
+
+// suffix basis: out[j] = in[j] + in[j + half] (Jacobian; normalised afterwards)
+__global__ __launch_bounds__(kBlock) void k_pair_sum(const G1A* __restrict__ in, uint64_t half, G1J* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < half; j += stride)
+    out[j] = g1_add_mixed(g1_from_affine(in[j]), in[j + half]);
+}
+
+// KZG quotient of the top variable: q[j] = f[j + half] - f[j] (get_quotient, kzg.rs:150-161)
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_top_diff(const Fe* __restrict__ f, uint64_t half, Fe* __restrict__ q) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < half; j += stride)
+    st_fe(q, j, fe_sub<F>(ld_fe(f, j + half), ld_fe(f, j)));
+}
+// f - v (poly_minus_v, kzg.rs:65-70)
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_sub_const(const Fe* __restrict__ f, uint64_t n, Fe v, Fe* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += stride)
+    st_fe(out, j, fe_sub<F>(ld_fe(f, j), v));
+}
+
+}  // namespace zk

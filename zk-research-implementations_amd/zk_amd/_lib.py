@@ -17,7 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer"]
+KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm"]
 
 
 class ZkError(RuntimeError):
@@ -28,10 +28,10 @@ class ZkError(RuntimeError):
 
 class ZkStats(C.Structure):
     _fields_ = [
-        ("launches", C.c_uint64 * 8),
-        ("kernel_ms", C.c_double * 8),
-        ("alg_bytes", C.c_double * 8),
-        ("field_muls", C.c_double * 8),
+        ("launches", C.c_uint64 * 9),
+        ("kernel_ms", C.c_double * 9),
+        ("alg_bytes", C.c_double * 9),
+        ("field_muls", C.c_double * 9),
         ("host_syncs", C.c_uint64),
         ("collectives", C.c_uint64),
         ("host_wait_us", C.c_double),
@@ -67,6 +67,13 @@ SIGNATURES = {
     "zk_gkr_circuit_rounds": (I, [U32, P, C.POINTER(U32)]),
     "zk_gkr_circuit_prove": (I, [P, I, I, U32, P, P, P, U32, P, P, P, P, P, P]),
     "zk_gkr_circuit_verify": (I, [I, I, U32, P, P, P, U32, P, P, P, P, P, C.POINTER(C.c_int)]),
+    "zk_kzg_setup": (I, [P, I, P, U32, C.POINTER(C.c_void_p)]),
+    "zk_kzg_free": (None, [P]),
+    "zk_kzg_lagrange_basis": (I, [P, P, U32, P]),
+    "zk_kzg_commit": (I, [P, P, I, P, P]),
+    "zk_dev_kzg_commit": (I, [P, P, P, P]),
+    "zk_kzg_get_proof": (I, [P, P, I, P, P, P, P]),
+    "zk_msm_g1": (I, [P, I, P, P, SZ, P]),
     "zk_gkr_proof_to_blob": (I, [I, I, P, P, U32, P, P, SZ, C.POINTER(SZ)]),
     "zk_sumcheck_proof_to_blob": (I, [I, I, P, U32, U32, P, P, SZ, C.POINTER(SZ)]),
     "zk_proof_blob_info": (I, [P, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(U32)]),

@@ -1,0 +1,95 @@
+"""Mirror of the reference multilinear KZG (pcs/src/kzg_pcs/kzg.rs) over
+BLS12-381 G1, on the GPU through the C ABI.
+
+Points are (x, y) canonical integers, None for the point at infinity (ark's
+affine identity). Scalars are BLS12-381 Fr integers. Not built: the G2 half of
+the trusted setup and the pairing-based KZG::verify (:97-129).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import lib
+from .api import Field, _call, default_context
+from .context import REPR_CANONICAL, Context
+from .elems import as_limbs, ptr, to_ints
+
+FIELD = Field.BLS12_381_FR
+
+
+def _points(a: np.ndarray) -> list:
+    out = []
+    for row in a:
+        x = sum(int(row[i]) << (64 * i) for i in range(6))
+        y = sum(int(row[6 + i]) << (64 * i) for i in range(6))
+        out.append(None if x == 0 and y == 0 else (x, y))
+    return out
+
+
+def _g1_array(points: list) -> np.ndarray:
+    a = np.zeros((max(len(points), 1), 12), np.uint64)
+    for k, pt in enumerate(points):
+        if pt is None:
+            continue
+        for j, v in enumerate(pt):
+            for i in range(6):
+                a[k, 6 * j + i] = (v >> (64 * i)) & 0xFFFFFFFFFFFFFFFF
+    return a
+
+
+class KZG:  # kzg.rs:10-49
+    def __init__(self, taus: list[int], ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        self.nvars = len(taus)
+        h = C.c_void_p()
+        _call(lib().zk_kzg_setup(self.ctx.h, REPR_CANONICAL, ptr(as_limbs([int(t) for t in taus])), self.nvars,
+                                 C.byref(h)))
+        self.h = h
+
+    def close(self) -> None:
+        if self.h:
+            lib().zk_kzg_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def lagrange_basis(self, nvars_suffix: int | None = None) -> list:  # get_lagrange_basis (:183-212)
+        v = self.nvars if nvars_suffix is None else nvars_suffix
+        out = np.zeros((1 << v, 12), np.uint64)
+        _call(lib().zk_kzg_lagrange_basis(self.ctx.h, self.h, v, ptr(out)))
+        return _points(out)
+
+    def commit(self, evals: list[int]):  # :51-53
+        out = np.zeros((1, 12), np.uint64)
+        _call(lib().zk_kzg_commit(self.ctx.h, self.h, REPR_CANONICAL, ptr(as_limbs([int(e) for e in evals])),
+                                  ptr(out)))
+        return _points(out)[0]
+
+    def open(self, opening_values: list[int], evals: list[int]) -> int:  # :55-57 (MultilinearPoly::evaluate)
+        res = np.zeros((1, 4), np.uint64)
+        pt = as_limbs([int(v) for v in opening_values])
+        _call(lib().zk_mle_evaluate(self.ctx.h, int(FIELD), REPR_CANONICAL, ptr(as_limbs([int(e) for e in evals])),
+                                    self.nvars, ptr(pt), len(opening_values), ptr(res)))
+        return to_ints(res)[0]
+
+    def get_proof(self, opened_value: int, opening_values: list[int], evals: list[int]) -> list:  # :59-95
+        out = np.zeros((self.nvars, 12), np.uint64)
+        _call(lib().zk_kzg_get_proof(self.ctx.h, self.h, REPR_CANONICAL, ptr(as_limbs([int(e) for e in evals])),
+                                     ptr(as_limbs([int(opened_value)])),
+                                     ptr(as_limbs([int(v) for v in opening_values])), ptr(out)))
+        return _points(out)
+
+
+def msm_g1(bases: list, scalars: list[int], ctx: Context | None = None):
+    """sum_i scalars[i] * bases[i] (bases must be on the curve)."""
+    ctx = ctx or default_context()
+    out = np.zeros((1, 12), np.uint64)
+    sc = as_limbs([int(s) for s in scalars]) if scalars else np.zeros((1, 4), np.uint64)
+    _call(lib().zk_msm_g1(ctx.h, REPR_CANONICAL, ptr(_g1_array(bases)), ptr(sc), len(scalars), ptr(out)))
+    return _points(out)[0]
