@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true")
     ap.add_argument("--no-circuit", action="store_true", help="skip the full GKR circuit prove (SURVEY 8(f2))")
+    ap.add_argument("--no-config5", action="store_true", help="skip BLS12-381 GKR + KZG commit (BASELINE config 5)")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
     return ap.parse_args()
 
@@ -147,6 +148,69 @@ def circuit_bench(ctx, field: int, log_inputs: int = 12, reps: int = 3) -> dict:
         "layer_kernels_ms_per_proof": k["ms"] / reps,
         "layer_tables_GBs": k["alg_bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] else None,
         "note": "the reference builds add_i/mul_i densely (2^(3g+2) entries: 2^35 at this size) and cannot run it",
+    }
+
+
+def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
+    """BASELINE config 5: the 24-variable GKR sum-check over BLS12-381 Fr, and
+    the KZG commitment of a 24-variable MLE over BLS12-381
+    G1: a 2^24-point Pippenger MSM against the Lagrange basis of fixed taus."""
+    import ctypes as C
+    import random
+
+    import numpy as np
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+    from zk_amd.elems import as_limbs, ptr
+    from zk_amd.kzg import KZG
+
+    field = 2
+    tabs = [ctx.synth(field, 1 << nvars, seed=5, table=t) for t in range(4)]
+    arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
+    coeffs = np.zeros((nvars, 3, 4), np.uint64)
+    nco = np.zeros(nvars, np.uint8)
+    ch = np.zeros((nvars, 4), np.uint64)
+    zero = ptr(as_limbs([0]))
+
+    def gkr():
+        tr = zk_amd.Transcript(field)
+        check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, nvars, 0, zero, tr.h, ptr(coeffs), ptr(nco),
+                                                      ptr(ch)))
+
+    gkr()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        gkr()
+        ts.append(time.perf_counter() - t0)
+    gkr_ms = sorted(ts)[reps // 2] * 1e3
+    del tabs
+    rng = random.Random(55)
+    taus = [rng.randrange(zk_amd.modulus(field)) for _ in range(nvars)]
+    t0 = time.perf_counter()
+    k = KZG(taus, ctx)
+    setup_ms = (time.perf_counter() - t0) * 1e3
+    evals = ctx.synth(field, 1 << nvars, seed=5, table=0)
+    out = np.zeros((1, 12), np.uint64)
+    check(lib().zk_dev_kzg_commit(ctx.h, k.h, evals.ptr, ptr(out)))  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        check(lib().zk_dev_kzg_commit(ctx.h, k.h, evals.ptr, ptr(out)))
+        ts.append(time.perf_counter() - t0)
+    commit_ms = sorted(ts)[reps // 2] * 1e3
+    k.close()
+    n = 1 << nvars
+    return {
+        "workload": f"BLS12-381: gkr_prove over {nvars} variables (A*S + M*P, seed 5) and the KZG commitment of a "
+                    f"{nvars}-variable MLE (2^{nvars}-point G1 MSM, Lagrange basis of fixed taus)",
+        "gkr_prove_ms": gkr_ms,
+        "gkr_field_ops_per_s": 32.0 * (n - 1) / (gkr_ms / 1e3),
+        "kzg_setup_ms": setup_ms,
+        "kzg_commit_ms": commit_ms,
+        "msm_points_per_s": n / (commit_ms / 1e3),
+        "note": "the reference commits with a naive sum of 2^24 full scalar multiplications (kzg.rs:131-144)",
     }
 
 
@@ -297,6 +361,8 @@ def main() -> None:
             out["fold_20var"] = fold_bench(ctx, field)
         if not args.no_circuit and world == 1:
             out["gkr_circuit"] = circuit_bench(ctx, field)
+        if not args.no_config5 and world == 1:
+            out["config5_bls12_381"] = config5_bench(ctx)
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(field, args.cpu_sample_nvars)
             out["cpu_baseline"] = cb
