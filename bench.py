@@ -357,7 +357,7 @@ def main() -> None:
                 "launches_by_kind": {kk: v["launches"] / args.steps for kk, v in k.items() if v["launches"]},
             },
         }
-        if not args.no_fold:
+        if not args.no_fold and world == 1:
             out["fold_20var"] = fold_bench(ctx, field)
         if not args.no_circuit and world == 1:
             out["gkr_circuit"] = circuit_bench(ctx, field)
