@@ -1,0 +1,324 @@
+// GKR over a layered circuit: host driver and C ABI.
+#include "host.hpp"
+
+using namespace zkh;
+
+namespace {
+// ---------------------------------------------------------------------------
+// GKR over a layered circuit: gkr_protocol.rs:31-126 with
+// every table-sized step on the device — circuit evaluation, the four layer
+// tables (kernels.hpp k_gate_weights / k_layer_tables, sparse wiring instead
+// of the reference's dense 2^(3g+2) add_i/mul_i), the layer sum-check
+// (gkr_prove_device) and w.evaluate(r_b / r_c) (mle_evaluate_device). The
+// transcript and O(1) scalar steps stay on the host, as in the reference.
+// Supported shape: the one for which the reference's table sizes agree — a
+// binary tree of layers, ninputs = 2 G_0, G_{l+1} = G_l / 2, powers of two,
+// output layer of 1 or 2 gates (initiate_protocol evaluates a 1-variable
+// output poly, :229-241). The input-layer KZG opening (row f3) is replaced by
+// returning the two input-MLE evaluations it opens (:106-111).
+// ---------------------------------------------------------------------------
+uint32_t lg2u(uint64_t x) {
+  uint32_t k = 0;
+  while (((uint64_t)1 << k) < x) ++k;
+  return k;
+}
+
+void check_shape(uint32_t nlayers, const uint32_t* gates) {
+  require(nlayers >= 1 && gates, "empty circuit");
+  require(nlayers <= 24, "too many layers");
+  for (uint32_t l = 0; l < nlayers; ++l) {
+    require(gates[l] >= 1 && (gates[l] & (gates[l] - 1)) == 0, "layer sizes must be powers of two");
+    if (l) require(2 * (uint64_t)gates[l] == gates[l - 1], "each layer must have half the gates of the one below");
+  }
+  require(gates[nlayers - 1] <= 2, "the output layer must have 1 or 2 gates");
+  require(lg2u(2 * (uint64_t)gates[0]) <= 14, "circuit too large (input layer tables of (2 G_0)^2 entries)");
+}
+
+void check_circuit(uint32_t nlayers, const uint32_t* gates, const uint8_t* ops, uint32_t ninputs) {
+  check_shape(nlayers, gates);
+  require(ops != nullptr, "null argument");
+  require((uint64_t)ninputs == 2 * (uint64_t)gates[0], "the first layer must have one gate per input pair");
+  size_t nops = 0;
+  for (uint32_t l = 0; l < nlayers; ++l) nops += gates[l];
+  for (size_t i = 0; i < nops; ++i) require(ops[i] <= 1, "gate op must be 0 (add) or 1 (mul)");
+}
+
+uint32_t circuit_rounds(uint32_t nlayers, const uint32_t* gates) {
+  uint32_t r = 0;
+  for (uint32_t l = 0; l < nlayers; ++l) r += 2 * lg2u(2 * (uint64_t)gates[l]);
+  return r;
+}
+
+struct CircuitOut {
+  Fe out_poly[2];
+  GkrOut sc;  // all layers' rounds, output layer first
+  std::vector<Fe> claims;
+  Fe in_eval[2];
+};
+
+template <class F>
+void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                              const zk_fe* inputs, uint32_t ninputs, CircuitOut& o) {
+  using namespace zk;
+  struct Scoped {
+    DevBuf b;
+    ~Scoped() { b.release(); }
+  } vals, dops, dwt, dpts;
+  std::vector<size_t> off(nlayers + 1), opoff(nlayers + 1);
+  off[0] = 0;
+  opoff[0] = 0;
+  for (uint32_t l = 0; l < nlayers; ++l) {
+    off[l + 1] = off[l] + (l == 0 ? ninputs : gates[l - 1]);
+    opoff[l + 1] = opoff[l] + gates[l];
+  }
+  const size_t nvals = off[nlayers] + gates[nlayers - 1];
+  vals.b.ensure(nvals * 32);
+  dops.b.ensure(opoff[nlayers]);
+  dwt.b.ensure((size_t)gates[0] * 32);
+  dpts.b.ensure(64 * 32);
+  upload<F>(c, repr, inputs, ninputs, vals.b.fe(0));
+  HIPCK(hipMemcpyAsync(dops.b.p, ops, opoff[nlayers], hipMemcpyHostToDevice, c->stream));
+  const uint8_t* dop = reinterpret_cast<const uint8_t*>(dops.b.p);
+  for (uint32_t l = 0; l < nlayers; ++l)  // Circuit::evaluate, input -> output (gkr_circuit.rs:127-143)
+    launch(c, ZK_K_LAYER, 96.0 * gates[l], 0.5 * gates[l], k_circuit_layer<F>, (gates[l] + kBlock - 1) / kBlock,
+           vals.b.fe(off[l]), dop + opoff[l], gates[l], vals.b.fe(off[l + 1]));
+  const uint32_t gout = gates[nlayers - 1];
+  Fe w0[2] = {fe_zero<F>(), fe_zero<F>()};
+  HIPCK(hipMemcpyAsync(w0, vals.b.fe(off[nlayers]), 32 * gout, hipMemcpyDeviceToHost, c->stream));
+  sync(c);  // (a 1-gate output is padded with zero, :36-38)
+  o.out_poly[0] = w0[0];
+  o.out_poly[1] = w0[1];
+
+  zk_transcript tr;  // Transcript::new() (:32)
+  absorb<F>(&tr, w0, 2);  // initiate_protocol (:229-241)
+  const Fe r0 = challenge<F>(&tr);
+  Fe claim = fe_add<F>(w0[0], fe_mul<F>(r0, fe_sub<F>(w0[1], w0[0])));
+  absorb<F>(&tr, &claim, 1);
+  std::vector<Fe> rb, rc;
+  Fe alpha = fe_zero<F>(), beta = fe_zero<F>();
+  const uint32_t total = circuit_rounds(nlayers, gates);
+  o.sc.coeffs.assign(3 * (size_t)total, fe_zero<F>());
+  o.sc.ncoeffs.assign(total, 0);
+  o.sc.challenges.assign(total, fe_zero<F>());
+  uint32_t k0 = 0;
+  for (uint32_t idx = 0; idx < nlayers; ++idx) {
+    const uint32_t l = nlayers - 1 - idx, G = gates[l], lgL = lg2u(2 * (uint64_t)G), nv = 2 * lgL;
+    const uint64_t T = (uint64_t)1 << nv;
+    const Fe* w = vals.b.fe(off[l]);  // the layer's inputs
+    // gate weights: output layer folds its 1-bit index with r0 (get_fbc_poly, :243-263);
+    // later layers alpha*eq(r_b, idx) + beta*eq(r_c, idx) (get_folded_fbc_poly, :265-292)
+    std::vector<Fe> pts;
+    uint32_t W;
+    Fe a = fe_one<F>(), b = fe_zero<F>();
+    uint32_t has_c = 0;
+    if (idx == 0) {
+      W = 1;
+      pts = {r0};
+    } else {
+      W = lg2u(G);
+      require(rb.size() == W && rc.size() == W, "internal: challenge split does not match the layer");
+      pts = rb;
+      pts.insert(pts.end(), rc.begin(), rc.end());
+      a = alpha;
+      b = beta;
+      has_c = 1;
+    }
+    HIPCK(hipMemcpyAsync(dpts.b.p, pts.data(), pts.size() * 32, hipMemcpyHostToDevice, c->stream));
+    launch(c, ZK_K_LAYER, 32.0 * G, (double)G * (W + 2), k_gate_weights<F>, (G + kBlock - 1) / kBlock, dpts.b.fe(0),
+           dpts.b.fe(W), W, a, b, has_c, G, dwt.b.fe(0));
+    c->input.ensure(4 * T * 32);
+    Fe* tab = c->input.fe();
+    const uint32_t grid = grid_for(c, T, k_layer_tables<F>);
+    launch(c, ZK_K_LAYER, 128.0 * T, (double)T, k_layer_tables<F>, grid, w, lgL, dwt.b.fe(0), dop + opoff[l], tab,
+           tab + T, tab + 2 * T, tab + 3 * T);
+    const Fe* dT[4] = {tab, tab + T, tab + 2 * T, tab + 3 * T};
+    GkrOut g;
+    gkr_prove_device<F>(c, dT, nv, false, &tr, g);  // gkr_prove(claimed_sum, &fbc_poly, &mut transcript) (:68)
+    for (uint32_t k = 0; k < nv; ++k) {
+      for (int i = 0; i < 3; ++i) o.sc.coeffs[3 * (size_t)(k0 + k) + i] = g.coeffs[3 * (size_t)k + i];
+      o.sc.ncoeffs[k0 + k] = g.ncoeffs[k];
+      o.sc.challenges[k0 + k] = g.challenges[k];
+    }
+    k0 += nv;
+    rb.assign(g.challenges.begin(), g.challenges.begin() + nv / 2);  // (:71-73)
+    rc.assign(g.challenges.begin() + nv / 2, g.challenges.end());
+    const Fe o1 = mle_evaluate_device<F>(c, w, lgL, rb), o2 = mle_evaluate_device<F>(c, w, lgL, rc);  // (:75-76)
+    if (idx + 1 < nlayers) {  // (:80-89)
+      absorb<F>(&tr, &o1, 1);
+      alpha = challenge<F>(&tr);
+      absorb<F>(&tr, &o2, 1);
+      beta = challenge<F>(&tr);
+      claim = fe_add<F>(fe_mul<F>(alpha, o1), fe_mul<F>(beta, o2));
+      o.claims.push_back(o1);
+      o.claims.push_back(o2);
+    } else {
+      o.in_eval[0] = o1;  // what KZG::open returns for r_b / r_c (:106-111)
+      o.in_eval[1] = o2;
+    }
+  }
+}
+
+// eq(pt, v) over n bits, MSB first (the multilinear extension of a point indicator)
+template <class F>
+Fe eq_bits(const Fe* pt, uint64_t v, uint32_t n) {
+  Fe e = zk::fe_one<F>();
+  for (uint32_t k = 0; k < n; ++k) {
+    const bool bit = (v >> (n - 1 - k)) & 1u;
+    e = zk::fe_mul<F>(e, bit ? pt[k] : zk::fe_sub<F>(zk::fe_one<F>(), pt[k]));
+  }
+  return e;
+}
+
+template <class F>
+Fe mle_eval_host(std::vector<Fe> t, const std::vector<Fe>& pt) {  // MultilinearPoly::evaluate (:79-91)
+  for (const Fe& r : pt) {
+    const size_t h = t.size() / 2;
+    for (size_t j = 0; j < h; ++j) t[j] = zk::fe_add<F>(t[j], zk::fe_mul<F>(r, zk::fe_sub<F>(t[j + h], t[j])));
+    t.resize(h);
+  }
+  return t[0];
+}
+
+// gkr::verify (gkr_protocol.rs:128-227). The wiring MLEs are evaluated
+// sparsely (one eq term per gate) — the same value as the reference's dense
+// add_i / mul_i evaluation. With inputs given, the input layer's two
+// evaluations are recomputed from them (standing in for the KZG checks).
+template <class F>
+bool gkr_circuit_verify_host(zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                             const zk_fe* inputs, uint32_t ninputs, const zk_fe* output_poly, const zk_fe* coeffs,
+                             const uint8_t* ncoeffs, const zk_fe* claims, const zk_fe* input_evals) {
+  using namespace zk;
+  std::vector<size_t> opoff(nlayers + 1, 0);
+  for (uint32_t l = 0; l < nlayers; ++l) opoff[l + 1] = opoff[l] + gates[l];
+  zk_transcript tr;
+  Fe w0[2] = {in_mont<F>(repr, output_poly[0]), in_mont<F>(repr, output_poly[1])};
+  absorb<F>(&tr, w0, 2);
+  const Fe r0 = challenge<F>(&tr);
+  Fe claim = fe_add<F>(w0[0], fe_mul<F>(r0, fe_sub<F>(w0[1], w0[0])));
+  absorb<F>(&tr, &claim, 1);
+  Fe alpha = fe_zero<F>(), beta = fe_zero<F>();
+  std::vector<Fe> prev;
+  std::vector<Fe> in_m;
+  if (inputs) {
+    in_m.resize(ninputs);
+    for (uint32_t i = 0; i < ninputs; ++i) in_m[i] = in_mont<F>(repr, inputs[i]);
+  }
+  size_t k0 = 0;
+  const Fe zero = fe_zero<F>(), one = fe_one<F>();
+  for (uint32_t idx = 0; idx < nlayers; ++idx) {
+    const uint32_t l = nlayers - 1 - idx, G = gates[l], lgL = lg2u(2 * (uint64_t)G), nv = 2 * lgL;
+    std::vector<Fe> chal;
+    for (uint32_t k = 0; k < nv; ++k) {  // gkr_verify (sum_check_protocol.rs:117-150)
+      const int m = ncoeffs[k0 + k];
+      require(m <= 3, "round polynomial has more than 3 coefficients");
+      Fe cf[3];
+      for (int i = 0; i < m; ++i) cf[i] = in_mont<F>(repr, coeffs[3 * (k0 + k) + i]);
+      auto ev = [&](const Fe& x) {
+        Fe s = zero, xp = one;
+        for (int i = 0; i < m; ++i) {
+          s = fe_add<F>(s, fe_mul<F>(cf[i], xp));
+          xp = fe_mul<F>(xp, x);
+        }
+        return s;
+      };
+      if (!fe_eq<F>(fe_add<F>(ev(zero), ev(one)), claim)) return false;
+      absorb<F>(&tr, cf, (size_t)m);
+      const Fe r = challenge<F>(&tr);
+      chal.push_back(r);
+      claim = ev(r);
+    }
+    k0 += nv;
+    Fe o1, o2;
+    if (idx + 1 == nlayers) {
+      o1 = in_mont<F>(repr, input_evals[0]);
+      o2 = in_mont<F>(repr, input_evals[1]);
+      if (inputs) {
+        const std::vector<Fe> rb(chal.begin(), chal.begin() + nv / 2), rc(chal.begin() + nv / 2, chal.end());
+        if (!fe_eq<F>(o1, mle_eval_host<F>(in_m, rb)) || !fe_eq<F>(o2, mle_eval_host<F>(in_m, rc))) return false;
+      }
+    } else {
+      o1 = in_mont<F>(repr, claims[2 * idx]);
+      o2 = in_mont<F>(repr, claims[2 * idx + 1]);
+    }
+    Fe a_r = zero, m_r = zero;
+    const uint32_t W = idx == 0 ? 1 : lg2u(G), Wbc = lgL;
+    for (uint32_t gi = 0; gi < G; ++gi) {
+      const uint64_t bc = ((uint64_t)(2 * gi) << Wbc) | (2 * gi + 1);
+      Fe wgt;
+      if (idx == 0) {  // get_verifier_claim: add_i.evaluate([r0] ++ chal) (:294-314)
+        std::vector<Fe> pt{r0};
+        pt.insert(pt.end(), chal.begin(), chal.end());
+        wgt = eq_bits<F>(pt.data(), ((uint64_t)gi << (2 * Wbc)) | bc, W + 2 * Wbc);
+      } else {  // get_folded_verifier_claim (:316-341)
+        const size_t mid = prev.size() / 2;
+        const Fe eb = eq_bits<F>(prev.data(), gi, W), ec = eq_bits<F>(prev.data() + mid, gi, W);
+        wgt = fe_mul<F>(fe_add<F>(fe_mul<F>(alpha, eb), fe_mul<F>(beta, ec)), eq_bits<F>(chal.data(), bc, 2 * Wbc));
+      }
+      if (ops[opoff[l] + gi]) m_r = fe_add<F>(m_r, wgt);
+      else a_r = fe_add<F>(a_r, wgt);
+    }
+    const Fe expect = fe_add<F>(fe_mul<F>(a_r, fe_add<F>(o1, o2)), fe_mul<F>(m_r, fe_mul<F>(o1, o2)));
+    if (!fe_eq<F>(expect, claim)) return false;
+    prev = chal;
+    absorb<F>(&tr, &o1, 1);
+    alpha = challenge<F>(&tr);
+    absorb<F>(&tr, &o2, 1);
+    beta = challenge<F>(&tr);
+    claim = fe_add<F>(fe_mul<F>(alpha, o1), fe_mul<F>(beta, o2));
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---- GKR over a layered circuit ----
+int zk_gkr_circuit_rounds(uint32_t nlayers, const uint32_t* gates, uint32_t* out_total_rounds) {
+  return guarded([&] {
+    require(gates && out_total_rounds, "null argument");
+    check_shape(nlayers, gates);
+    *out_total_rounds = circuit_rounds(nlayers, gates);
+  });
+}
+
+int zk_gkr_circuit_prove(zk_ctx* c, zk_field field, zk_repr repr, uint32_t nlayers, const uint32_t* gates,
+                         const uint8_t* ops, const zk_fe* inputs, uint32_t ninputs, zk_fe* out_output_poly,
+                         zk_fe* out_coeffs, uint8_t* out_ncoeffs, zk_fe* out_challenges, zk_fe* out_claims,
+                         zk_fe* out_input_evals) {
+  return guarded([&] {
+    require(c && inputs && out_output_poly && out_coeffs && out_ncoeffs && out_challenges && out_input_evals,
+            "null argument");
+    check_circuit(nlayers, gates, ops, ninputs);
+    require(nlayers == 1 || out_claims, "null argument");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      CircuitOut o;
+      gkr_circuit_prove_device<F>(c, repr, nlayers, gates, ops, inputs, ninputs, o);
+      for (int i = 0; i < 2; ++i) out_output_poly[i] = out_repr<F>(repr, o.out_poly[i]);
+      emit_gkr<F>(repr, o.sc, (uint32_t)o.sc.ncoeffs.size(), out_coeffs, out_ncoeffs, out_challenges);
+      for (size_t i = 0; i < o.claims.size(); ++i) out_claims[i] = out_repr<F>(repr, o.claims[i]);
+      for (int i = 0; i < 2; ++i) out_input_evals[i] = out_repr<F>(repr, o.in_eval[i]);
+    });
+  });
+}
+
+int zk_gkr_circuit_verify(zk_field field, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                          const zk_fe* inputs, uint32_t ninputs, const zk_fe* output_poly, const zk_fe* coeffs,
+                          const uint8_t* ncoeffs, const zk_fe* claims, const zk_fe* input_evals, int* out_verified) {
+  return guarded([&] {
+    require(output_poly && coeffs && ncoeffs && input_evals && out_verified, "null argument");
+    check_circuit(nlayers, gates, ops, ninputs);
+    require(nlayers == 1 || claims, "null argument");
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      *out_verified = gkr_circuit_verify_host<F>(repr, nlayers, gates, ops, inputs, ninputs, output_poly, coeffs,
+                                                 ncoeffs, claims, input_evals)
+                          ? 1
+                          : 0;
+    });
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,752 @@
+// Host-side core shared by the library's translation units (zk_sumcheck.hip,
+// gkr_circuit.hip, kzg.hip, blob.hip): errors and the C-ABI guard, field
+// dispatch and representation conversion, the transcript, the device context
+// (zk_ctx), kernel launch / timing, and the sum-check / GKR round drivers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/zk_sumcheck.h"
+#include "field.hpp"
+#include "keccak.hpp"
+#include "kernels.hpp"
+
+using zk::Fe;
+
+// ===========================================================================
+// errors
+// ===========================================================================
+namespace zkh {
+inline thread_local std::string g_last_error;
+
+struct ZkError {
+  int code;
+  std::string msg;
+};
+[[noreturn]] inline void fail(int code, const std::string& msg) { throw ZkError{code, msg}; }
+
+#define HIPCK(x)                                                                        \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) fail(ZK_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define NCCLCK(x)                                                                            \
+  do {                                                                                       \
+    ncclResult_t r_ = (x);                                                                   \
+    if (r_ != ncclSuccess) fail(ZK_ECOMM, std::string(#x) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+template <class Fn>
+int guarded(Fn&& fn) {
+  try {
+    fn();
+    g_last_error.clear();
+    return ZK_OK;
+  } catch (const ZkError& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return ZK_ENOMEM;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return ZK_EDEVICE;
+  }
+}
+
+inline void require(bool cond, const char* msg) {
+  if (!cond) fail(ZK_EINVAL, msg);
+}
+
+// runtime field -> compile-time parameter set
+template <class Fn>
+void dispatch(zk_field field, Fn&& fn) {
+  switch (field) {
+    case ZK_BN254_FR: fn(zk::Bn254Fr{}); break;
+    case ZK_BN254_FQ: fn(zk::Bn254Fq{}); break;
+    case ZK_BLS12_381_FR: fn(zk::Bls12_381Fr{}); break;
+    default: fail(ZK_EINVAL, "unknown field");
+  }
+}
+
+// zk_fe (4 x u64 LE) <-> Fe (8 x u32 LE): same bytes on a little-endian host
+inline Fe from_zk(const zk_fe& a) {
+  Fe r;
+  memcpy(r.v, a.limb, 32);
+  return r;
+}
+inline zk_fe to_zk(const Fe& a) {
+  zk_fe r;
+  memcpy(r.limb, a.v, 32);
+  return r;
+}
+
+template <class F>
+Fe in_mont(zk_repr repr, const zk_fe& a) {  // host scalar in -> Montgomery
+  Fe x = from_zk(a);
+  require(zk::fe_is_canonical<F>(x), "field element >= modulus");
+  return repr == ZK_REPR_MONTGOMERY ? x : zk::fe_to_mont<F>(x);
+}
+template <class F>
+zk_fe out_repr(zk_repr repr, const Fe& m) {  // Montgomery -> host scalar out
+  return to_zk(repr == ZK_REPR_MONTGOMERY ? m : zk::fe_from_mont<F>(m));
+}
+template <class F>
+void canon_bytes(const Fe& m, uint8_t out[32]) {  // into_bigint().to_bytes_le()
+  const Fe c = zk::fe_from_mont<F>(m);
+  memcpy(out, c.v, 32);
+}
+
+}  // namespace zkh
+using namespace zkh;
+
+// ===========================================================================
+// transcript (fiat_shamir_transcript.rs:5-37)
+// ===========================================================================
+struct zk_transcript {
+  zk::Keccak256 h;
+};
+
+namespace zkh {
+// get_random_challenge: d = finalize_reset(); append(d); from_le_bytes_mod_order(d)
+template <class F>
+Fe challenge(zk_transcript* t) {
+  uint8_t d[32];
+  t->h.finalize_reset(d);
+  t->h.update(d, 32);
+  Fe x;
+  memcpy(x.v, d, 32);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) x = zk::fe_reduce_once<F>(x);  // 2^256 < 6p
+  return zk::fe_to_mont<F>(x);
+}
+template <class F>
+void absorb(zk_transcript* t, const Fe* m, size_t n) {  // append(fq_vec_to_bytes(v))
+  uint8_t b[32];
+  for (size_t i = 0; i < n; ++i) {
+    canon_bytes<F>(m[i], b);
+    t->h.update(b, 32);
+  }
+}
+}  // namespace zkh
+using namespace zkh;
+
+// ===========================================================================
+// context
+// ===========================================================================
+namespace zkh {
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes) return;
+    if (p) HIPCK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, b) != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      fail(ZK_ENOMEM, "hipMalloc of " + std::to_string(b) + " bytes failed");
+    }
+    bytes = b;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  Fe* fe(size_t off_elems = 0) const { return reinterpret_cast<Fe*>(p) + off_elems; }
+};
+
+enum CommKind { COMM_NONE = 0, COMM_HOST = 1, COMM_RCCL = 2 };
+}  // namespace zkh
+using namespace zkh;
+
+struct zk_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  DevBuf work[2];  // ping-pong fold workspaces: 4 tables each
+  DevBuf input;    // host-API staging (4 tables)
+  DevBuf partials;
+  DevBuf small;    // round totals (<= 64 u64) + flag + gather buffers
+  uint64_t* h_red = nullptr;  // pinned, device-mapped: round totals (<= 51 u64) + flag word at [64]
+  uint32_t tag = 0;           // last round tag handed to a kernel
+  uint64_t lanes_max_pairs = 1u << 15;  // rounds with <= this many pairs use 8 lanes per pair
+  std::chrono::steady_clock::time_point work_t0;  // when the last round result was seen
+  bool work_open = false;
+  uint32_t timing = 0;  // bit k: time launches of kernel kind k
+  zk_stats stats{};
+  struct Pending {
+    int kind;
+    hipEvent_t a, b;
+  };
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free;
+  std::vector<Pending> pending;
+  // communicator
+  int rank = 0, world = 1;
+  CommKind comm = COMM_NONE;
+  zk_allreduce_u64_fn ar = nullptr;
+  bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
+  bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
+  uint32_t rtag = 0;        // last tag handed to a pre-enqueued round kernel
+  void* user = nullptr;
+  ncclComm_t nccl = nullptr;
+  // KZG / MSM scratch (grow-only) and the cached fixed-base table of G1
+  DevBuf msm[16];
+  DevBuf scan_tmp[4];
+  DevBuf g1_table;
+};
+
+
+namespace zkh {
+// small device area: [0,512) round sums, [512] input check flag, [1024,2304)
+// fan-in counters (9 x 128 B), [2560,3072) limb accumulator (<= 64 u64),
+// [4096, +64 KiB) all-reduce bounce buffer
+// (<= 256 ranks x 256 B), then the tail's 4 local elements and the gathered
+// 4 x world tables
+constexpr size_t kSmallBytes = 160 * 1024;
+inline uint64_t* d_red(zk_ctx* c) { return reinterpret_cast<uint64_t*>(c->small.p); }
+inline uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 512); }
+inline uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 1024); }
+inline uint64_t* d_accum(zk_ctx* c) { return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(c->small.p) + 2560); }
+inline uint32_t* h_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(c->h_red + 64); }
+inline char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 4096; }
+// pre-enqueued rounds: the pinned slot the host posts r to, the pinned error
+// word, and the device relay slots (h_red page: [1024, 1088) and [2048];
+// small area: [3072, 3584) = 8 x 64 B)
+inline zk::RWait* h_rin(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->h_red) + 1024); }
+inline uint32_t* h_err(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->h_red) + 2048); }
+inline zk::RWait* d_relay(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->small.p) + 3072); }
+
+inline void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
+
+// At most one resident wave of 256-thread blocks (blocks/CU from the
+// kernel's register budget), grid-striding over the rest: no tail of
+// half-empty CUs.
+template <class K>
+uint32_t grid_for(zk_ctx* c, uint64_t work, K kernel) {
+  static thread_local std::vector<std::pair<const void*, int>> cache;
+  int per_cu = 0;
+  for (auto& e : cache)
+    if (e.first == reinterpret_cast<const void*>(kernel)) per_cu = e.second;
+  if (per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, zk::kBlock, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    cache.push_back({reinterpret_cast<const void*>(kernel), per_cu});
+  }
+  const uint64_t cap = (uint64_t)c->num_cus * per_cu;
+  uint64_t g = (work + zk::kBlock - 1) / zk::kBlock;
+  if (g < 1) g = 1;
+  return (uint32_t)std::min<uint64_t>(g, cap);
+}
+
+// Launch wrapper: counts algorithmic bytes / multiplications per kernel kind
+// and, when timing is on, has the dispatch packet itself record start/stop
+// events on c->stream (hipExtLaunchKernelGGL: no extra API calls per launch).
+template <class Kern, class... Args>
+void launch(zk_ctx* c, int kind, double bytes, double muls, Kern kernel, uint32_t grid, Args... args) {
+  zk_ctx::Pending p{kind, nullptr, nullptr};
+  const bool timed = (c->timing >> kind) & 1u;
+  if (timed) {
+    if (c->ev_free.empty()) {
+      hipEvent_t a, b;
+      HIPCK(hipEventCreate(&a));
+      HIPCK(hipEventCreate(&b));
+      c->ev_free.push_back({a, b});
+    }
+    p.a = c->ev_free.back().first;
+    p.b = c->ev_free.back().second;
+    c->ev_free.pop_back();
+  }
+  hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(zk::kBlock), 0, c->stream, p.a, p.b, 0, args...);
+  HIPCK(hipGetLastError());
+  if (c->work_open) {
+    c->stats.host_work_us +=
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->work_t0).count();
+    c->work_open = false;
+  }
+  if (timed) c->pending.push_back(p);
+  c->stats.launches[kind] += 1;
+  c->stats.alg_bytes[kind] += bytes;
+  c->stats.field_muls[kind] += muls;
+}
+// after a stream sync: fold event timings into the stats
+inline void flush_timing(zk_ctx* c) {
+  static const bool dbg = getenv("ZK_DEBUG_EVENTS") != nullptr;
+  for (auto& p : c->pending) {
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
+    if (dbg) fprintf(stderr, "zk: kind %d %.1f us\n", p.kind, ms * 1e3);
+    c->stats.kernel_ms[p.kind] += ms;
+    c->ev_free.push_back({p.a, p.b});
+  }
+  c->pending.clear();
+}
+inline void sync(zk_ctx* c) {
+  c->work_open = false;
+  HIPCK(hipStreamSynchronize(c->stream));
+  c->stats.host_syncs += 1;
+  flush_timing(c);
+}
+
+// limb-split element sum (8 x u64 holding 32-bit limbs, possibly summed over
+// ranks) -> field element (Montgomery image of the sum)
+template <class F>
+Fe from_limb_sums(const uint64_t* w) {
+  return zk::limbs_to_fe<F>(w, 8, false);
+}
+
+// ---------------------------------------------------------------------------
+// Round sums: the round kernel's last block writes the K sums (limb-split)
+// straight into pinned host memory and raises a flag; the host spins on the
+// flag (no stream synchronisation, no copy kernel). Across ranks over RCCL the
+// sums go to device memory, are all-reduced on the stream, then published.
+// ---------------------------------------------------------------------------
+inline bool multi_rank(zk_ctx* c) { return (c->world > 1 || c->force_coll) && c->comm != COMM_NONE; }
+
+// In-place SUM of n u64 over all ranks (host memory in/out). RCCL runs on the
+// ctx stream through a device bounce buffer; a host communicator runs its callback.
+inline void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
+  if (c->comm == COMM_RCCL) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(d_gather(c));
+    HIPCK(hipMemcpyAsync(d, w, n * 8, hipMemcpyHostToDevice, c->stream));
+    NCCLCK(ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, c->stream));
+    HIPCK(hipMemcpyAsync(w, d, n * 8, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+  } else if (c->comm == COMM_HOST) {
+    if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+  } else {
+    fail(ZK_ECOMM, "no communicator attached");
+  }
+  c->stats.collectives += 1;
+}
+
+inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
+  zk::RoundSink s;
+  s.partials = reinterpret_cast<uint64_t*>(c->partials.p);
+  s.counter = d_counter(c);
+  s.accum = d_accum(c);
+  s.tag = ++c->tag;
+  const bool via_rccl = across_ranks && multi_rank(c) && c->comm == COMM_RCCL;
+  s.dev_out = via_rccl ? d_red(c) : nullptr;
+  s.host_out = via_rccl ? nullptr : c->h_red;
+  s.host_flag = via_rccl ? nullptr : h_flag(c);
+  return s;
+}
+
+inline void wait_flag(zk_ctx* c, uint32_t tag) {
+  const uint32_t* f = h_flag(c);
+  uint64_t spins = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (c->work_open) {  // host work since the previous result ends at this wait
+    c->stats.host_work_us += std::chrono::duration<double, std::micro>(t0 - c->work_t0).count();
+    c->work_open = false;
+  }
+  while (__atomic_load_n(f, __ATOMIC_ACQUIRE) != tag) {
+    __builtin_ia32_pause();
+    if ((++spins & 0xFFFF) == 0) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) fail(ZK_EDEVICE, std::string("round kernel failed: ") + hipGetErrorString(e));
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if ((e == hipSuccess && s > 1.0) || s > 60.0) fail(ZK_EDEVICE, "round result flag never arrived");
+    }
+  }
+  c->work_t0 = std::chrono::steady_clock::now();
+  c->work_open = true;
+  c->stats.host_wait_us += std::chrono::duration<double, std::micro>(c->work_t0 - t0).count();
+  c->stats.host_syncs += 1;
+}
+
+// The round kernel's totals: K values of L limb sums each (L = 17: unreduced
+// product sums, L = 8: element sums), summed over ranks when sharded.
+// Stream side of a round's hand-off, enqueued right after its kernel: across
+// ranks over RCCL the device totals are all-reduced and then published.
+inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
+  if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
+    NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
+    c->stats.collectives += 1;
+    zk::k_publish<<<1, 64, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
+    HIPCK(hipGetLastError());
+  }
+}
+
+template <class F, int K>
+void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
+  const bool multi = across_ranks && multi_rank(c);
+  const int n = K * L;
+  wait_flag(c, sk.tag);
+  if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) != 0)
+    fail(ZK_EDEVICE, "a pre-enqueued round kernel waited more than 1 s for its challenge");
+  uint64_t w[K * 17];
+  for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
+  if (multi && c->comm == COMM_HOST) {
+    if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+    c->stats.collectives += 1;
+  }
+  for (int k = 0; k < K; ++k) out[k] = zk::limbs_to_fe<F>(w + L * k, L, L == 17);
+}
+
+inline void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kSlotU64 * 8); }
+
+// ---------------------------------------------------------------------------
+// GKR sum-check rounds
+// ---------------------------------------------------------------------------
+struct GkrOut {
+  std::vector<Fe> coeffs;     // 3 per round (Montgomery), trimmed count in ncoeffs
+  std::vector<uint8_t> ncoeffs;
+  std::vector<Fe> challenges;
+};
+
+// Round polynomial through (0,e0),(1,e1),(2,e2) — the unique degree<=2
+// polynomial UnivariatePoly::interpolate returns (univariate_polynomial_dense.rs:48-74),
+// trailing zero coefficients trimmed (:14-18). Absorbs it, draws r_k and
+// returns s_k(r_k).
+template <class F>
+Fe finish_round(zk_transcript* tr, const Fe& e0, const Fe& e1, const Fe& e2, uint32_t k, GkrOut& out, Fe& r) {
+  using namespace zk;
+  Fe c[3];
+  c[0] = e0;
+  c[2] = fe_mul<F>(fe_add<F>(fe_sub<F>(e0, fe_dbl<F>(e1)), e2), fe_inv2<F>());
+  c[1] = fe_sub<F>(fe_sub<F>(e1, e0), c[2]);
+  int m = 3;
+  while (m > 0 && fe_is_zero<F>(c[m - 1])) --m;
+  absorb<F>(tr, c, (size_t)m);
+  out.ncoeffs[k] = (uint8_t)m;
+  for (int i = 0; i < 3; ++i) out.coeffs[3 * k + i] = i < m ? c[i] : fe_zero<F>();
+  r = challenge<F>(tr);
+  out.challenges[k] = r;
+  // UnivariatePoly::evaluate(r) (:20-26) via Horner — same field value
+  return fe_add<F>(c[0], fe_mul<F>(r, fe_add<F>(c[1], fe_mul<F>(r, c[2]))));
+}
+
+// Posts the challenge of a finished round to the pinned slot the next
+// pre-enqueued round kernel polls. If the host unwinds mid-proof (exception),
+// the destructor posts the last tag (kernels compare with >=, so every round
+// still waiting proceeds with r = 0; its results are discarded) and drains
+// the stream, so no kernel is left waiting.
+struct PostR {
+  zk_ctx* c;
+  uint32_t last = 0;  // highest tag a kernel of this phase waits for (0: none)
+  bool done = false;
+  void post(const Fe& r, uint32_t tag) {
+    zk::RWait* s = h_rin(c);
+    for (int i = 0; i < 8; ++i) __atomic_store_n(&s->r.v[i], r.v[i], __ATOMIC_RELAXED);
+    __atomic_store_n(&s->tag, tag, __ATOMIC_RELEASE);
+  }
+  ~PostR() {
+    if (done || last == 0) return;
+    post(zk::fe_zero<zk::Bn254Fr>(), last);
+    (void)hipStreamSynchronize(c->stream);
+  }
+};
+
+// Pre-enqueue the rounds of a phase (ZK_PRELAUNCH, default on)?
+inline bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1; }
+
+// Run `nv` rounds over 4 device tables of 2^nv elements starting at global
+// round k0. The first round of a phase computes e0,e1,e2 directly; later
+// rounds fold by the previous challenge in the same kernel. On return `cur`
+// points at the (unfolded) size-2 tables of the last round.
+// Pre-enqueued (default): every round kernel (and, across ranks over RCCL,
+// its all-reduce + publish) is enqueued before round 0's sums are read;
+// round i's kernel waits in-kernel for r_{i-1}, which the host posts as soon
+// as it has run the transcript. Otherwise each round is launched after the
+// previous challenge is known.
+template <class F>
+void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
+               GkrOut& out, Fe& claim, Fe& r) {
+  const uint64_t L = (uint64_t)1 << nv;
+  const bool pre = prelaunch(c, nv);
+  std::vector<zk::RoundSink> sinks(nv);
+  std::vector<uint32_t> rtags(nv, 0);
+  auto enqueue = [&](uint32_t i) {
+    const uint64_t size = L >> i;  // table length in this round
+    const uint64_t h = size / 2;   // pairs
+    sinks[i] = make_sink(c, across_ranks);
+    const zk::RoundSink& sk = sinks[i];
+    if (i == 0) {
+      const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round0<F>);
+      launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, zk::k_gkr_round0<F>, grid, cur[0], cur[1], cur[2], cur[3], h, sk);
+      enqueue_reduce(c, sk, across_ranks, 3 * 17);
+      return;
+    }
+    // fold previous (size 2*size) -> work[(i+1)&1] (size `size`) and evaluate;
+    // work[0] holds the size-L/2 level, work[1] the size-L/4 level, ...
+    Fe* w = c->work[(i + 1) & 1].fe();
+    Fe* nx[4] = {w, w + size, w + 2 * size, w + 3 * size};
+    zk::RoundIn rin{};
+    if (pre) {
+      rin.host = h_rin(c);
+      rin.relay = d_relay(c);
+      rin.err = h_err(c);
+      rin.tag = rtags[i] = ++c->rtag;
+    } else {
+      rin.r = r;
+    }
+    if (h <= c->lanes_max_pairs) {  // latency-bound size: 8 lanes per pair
+      const uint32_t g8 = grid_for(c, 8 * h, zk::k_gkr_round_lanes<F>);
+      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round_lanes<F>, g8, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
+    } else {
+      const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round<F>);
+      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
+    }
+    for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+    enqueue_reduce(c, sk, across_ranks, 2 * 17);
+  };
+  PostR post{c};
+  if (pre) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; i < nv; ++i) {
+      enqueue(i);
+      post.last = rtags[i];  // from here on the guard releases what is enqueued
+    }
+    if (getenv("ZK_DEBUG_ENQUEUE"))
+      fprintf(stderr, "zk: enqueued %u rounds in %.1f us\n", nv,
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+  for (uint32_t i = 0; i < nv; ++i) {
+    const uint32_t k = k0 + i;
+    if (!pre) enqueue(i);
+    Fe e0, e1, e2;
+    if (i == 0) {
+      Fe s[3];
+      collect_sums<F, 3>(c, sinks[i], across_ranks, 17, s);
+      e0 = s[0];
+      e1 = s[1];
+      e2 = s[2];
+    } else {
+      Fe s[2];
+      collect_sums<F, 2>(c, sinks[i], across_ranks, 17, s);
+      e0 = s[0];
+      e2 = s[1];
+      // s_{k-1}(X) = sum_j f(X, j) is exact (degree 2 in X), so
+      // e0 + e1 = s_{k-1}(r_{k-1}) on the folded tables.
+      e1 = zk::fe_sub<F>(claim, e0);
+    }
+    claim = finish_round<F>(tr, e0, e1, e2, k, out, r);
+    if (pre && i + 1 < nv) post.post(r, rtags[i + 1]);
+  }
+  post.done = true;
+}
+
+template <class F>
+void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool sharded, zk_transcript* tr, GkrOut& out) {
+  const int G = sharded ? c->world : 1;
+  uint32_t lg = 0;
+  while ((1 << lg) < G) ++lg;
+  const uint32_t n = nloc + lg;
+  out.coeffs.assign(3 * (size_t)n, zk::fe_zero<F>());
+  out.ncoeffs.assign(n, 0);
+  out.challenges.assign(n, zk::fe_zero<F>());
+  if (n == 0) return;
+  ensure_partials(c);
+  __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
+  const uint64_t Lloc = (uint64_t)1 << nloc;
+  const uint64_t wmax = std::max<uint64_t>(Lloc / 2, (uint64_t)G);
+  c->work[0].ensure(4 * wmax * 32);
+  c->work[1].ensure(4 * std::max<uint64_t>(wmax / 2, 1) * 32);
+  const Fe* cur[4] = {dT[0], dT[1], dT[2], dT[3]};
+  Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
+  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r);
+  if (lg == 0) {
+    sync(c);  // settles event timings; the results are already on the host
+    return;
+  }
+
+  // ---- multi-GPU tail: every rank now holds 1 (folded) element per table ----
+  // Gather the G x 4 elements with the same exact all-reduce as the rounds:
+  // each rank fills only its own slot of a zeroed limb-split vector.
+  Fe* send = reinterpret_cast<Fe*>(d_gather(c) + 65536);  // 4 elements, after the bounce buffer
+  if (nloc > 0) {
+    Fe* s4[4] = {send, send + 1, send + 2, send + 3};
+    launch(c, ZK_K_FOLD, 4 * 96.0, 4.0, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], s4[0], s4[1], s4[2],
+           s4[3], (uint64_t)1, r);
+  } else {
+    for (int t = 0; t < 4; ++t) HIPCK(hipMemcpyAsync(send + t, cur[t], 32, hipMemcpyDeviceToDevice, c->stream));
+  }
+  Fe mine[4];
+  HIPCK(hipMemcpyAsync(mine, send, 128, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  std::vector<uint64_t> w((size_t)G * 4 * 8, 0);
+  for (int t = 0; t < 4; ++t)
+    for (int i = 0; i < 8; ++i) w[((size_t)c->rank * 4 + t) * 8 + i] = mine[t].v[i];
+  allreduce_host(c, w.data(), w.size());
+  // global table t, index g = rank g's element (local index 0 <-> global g)
+  std::vector<Fe> tabs((size_t)4 * G);
+  for (int g = 0; g < G; ++g)
+    for (int t = 0; t < 4; ++t) tabs[(size_t)t * G + g] = from_limb_sums<F>(&w[((size_t)g * 4 + t) * 8]);
+  Fe* stage = send + 4;
+  HIPCK(hipMemcpyAsync(stage, tabs.data(), tabs.size() * 32, hipMemcpyHostToDevice, c->stream));
+  const Fe* tcur[4] = {stage, stage + G, stage + 2 * G, stage + 3 * G};
+  gkr_phase<F>(c, tcur, lg, nloc, false, tr, out, claim, r);
+  sync(c);
+}
+
+// ---------------------------------------------------------------------------
+// plain sum-check
+// ---------------------------------------------------------------------------
+template <class F>
+void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, const uint8_t* table_bytes,
+                     size_t nbytes, Fe* rp, Fe& claimed) {
+  // The transcript absorbs the whole table first (sum_check_protocol.rs:27):
+  // a serial host Keccak. Round 0's half sums (and, pre-enqueued, every later
+  // round) are launched before it so the GPU works underneath the hash.
+  ensure_partials(c);
+  __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
+  const uint64_t N = (uint64_t)1 << n;
+  if (n == 0) {
+    tr->h.update(table_bytes, nbytes);
+    HIPCK(hipMemcpyAsync(&claimed, dX, 32, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    absorb<F>(tr, &claimed, 1);
+    return;
+  }
+  c->work[0].ensure(std::max<uint64_t>(N / 2, 1) * 32);
+  c->work[1].ensure(std::max<uint64_t>(N / 4, 1) * 32);
+  const bool pre = prelaunch(c, n);
+  std::vector<zk::RoundSink> sinks(n);
+  std::vector<uint32_t> rtags(n, 0);
+  const Fe* cur = dX;
+  Fe r = zk::fe_zero<F>();
+  auto enqueue = [&](uint32_t k) {
+    sinks[k] = make_sink(c, false);
+    zk::RoundIn rin{};
+    if (k == 0) {
+      const uint64_t h = N / 2;
+      const uint32_t grid = grid_for(c, h, zk::k_sc_round<F, true>);
+      launch(c, ZK_K_SC_ROUND, 64.0 * h, 0, zk::k_sc_round<F, true>, grid, dX, nullptr, h, rin, sinks[k]);
+      return;
+    }
+    const uint64_t h = (N >> k) / 2;
+    const uint32_t grid = grid_for(c, h, zk::k_sc_round<F, false>);
+    Fe* nx = c->work[(k + 1) & 1].fe();
+    if (pre) {
+      rin.host = h_rin(c);
+      rin.relay = d_relay(c);
+      rin.err = h_err(c);
+      rin.tag = rtags[k] = ++c->rtag;
+    } else {
+      rin.r = r;
+    }
+    launch(c, ZK_K_SC_ROUND, 192.0 * h, 2.0 * h, zk::k_sc_round<F, false>, grid, cur, nx, h, rin, sinks[k]);
+    cur = nx;
+  };
+  PostR post{c};
+  if (pre)
+    for (uint32_t k = 0; k < n; ++k) {
+      enqueue(k);
+      post.last = rtags[k];
+    }
+  else
+    enqueue(0);
+  tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps the GPU
+  for (uint32_t k = 0; k < n; ++k) {
+    if (!pre && k > 0) enqueue(k);
+    Fe s[2];
+    collect_sums<F, 2>(c, sinks[k], false, 8, s);
+    if (k == 0) {
+      claimed = zk::fe_add<F>(s[0], s[1]);  // = sum of the table (:29)
+      absorb<F>(tr, &claimed, 1);
+    }
+    rp[2 * k] = s[0];
+    rp[2 * k + 1] = s[1];
+    absorb<F>(tr, s, 2);
+    r = challenge<F>(tr);
+    if (pre && k + 1 < n) post.post(r, rtags[k + 1]);
+  }
+  post.done = true;
+  sync(c);
+}
+
+// MultilinearPoly::evaluate on device: n folds at bit 0, ping-pong workspaces
+template <class F>
+Fe mle_evaluate_device(zk_ctx* c, const Fe* dX, uint32_t n, const std::vector<Fe>& pt) {
+  const uint64_t N = (uint64_t)1 << n;
+  Fe res;
+  if (n == 0) {
+    HIPCK(hipMemcpyAsync(&res, dX, 32, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    return res;
+  }
+  c->work[0].ensure(std::max<uint64_t>(N / 2, 1) * 32);
+  c->work[1].ensure(std::max<uint64_t>(N / 4, 1) * 32);
+  const Fe* cur = dX;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t half = N >> (i + 1);
+    Fe* nx = c->work[i & 1].fe();
+    const uint32_t grid = grid_for(c, half, zk::k_fold<F>);
+    const Fe r = pt[i];
+    const uint32_t s = n - 1 - i;  // bit 0 of the current (n-i)-variable table
+    launch(c, ZK_K_FOLD, 96.0 * half, (double)half, zk::k_fold<F>, grid, cur, nx, half, s, r);
+    cur = nx;
+  }
+  HIPCK(hipMemcpyAsync(&res, cur, 32, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  return res;
+}
+
+// ---------------------------------------------------------------------------
+// host <-> device staging with representation conversion
+// ---------------------------------------------------------------------------
+template <class F>
+void upload(zk_ctx* c, zk_repr repr, const zk_fe* host, size_t n, Fe* dev) {
+  if (n == 0) return;
+  HIPCK(hipMemcpyAsync(dev, host, n * 32, hipMemcpyHostToDevice, c->stream));
+  HIPCK(hipMemsetAsync(d_flag(c), 0, 4, c->stream));
+  const uint32_t grid = grid_for(c, n, zk::k_check_canonical<F>);
+  launch(c, ZK_K_CONVERT, 32.0 * n, 0, zk::k_check_canonical<F>, grid, dev, n, d_flag(c));
+  if (repr == ZK_REPR_CANONICAL)
+    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n, zk::k_convert<F, true>, grid, dev, dev, n);
+  uint32_t bad = 0;
+  HIPCK(hipMemcpyAsync(&bad, d_flag(c), 4, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  require(bad == 0, "field element >= modulus in input table");
+}
+template <class F>
+void download(zk_ctx* c, zk_repr repr, const Fe* dev, size_t n, zk_fe* host) {
+  if (n == 0) return;
+  if (repr == ZK_REPR_CANONICAL) {
+    c->work[1].ensure(std::max(c->work[1].bytes, n * 32));
+    Fe* tmp = c->work[1].fe();
+    const uint32_t grid = grid_for(c, n, zk::k_convert<F, false>);
+    launch(c, ZK_K_CONVERT, 64.0 * n, (double)n, zk::k_convert<F, false>, grid, dev, tmp, n);
+    dev = tmp;
+  }
+  HIPCK(hipMemcpyAsync(host, dev, n * 32, hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+}
+
+// canonical table bytes for the plain-prove transcript (fq_vec_to_bytes)
+template <class F>
+std::vector<uint8_t> table_bytes_from_device(zk_ctx* c, const Fe* dev, size_t n) {
+  std::vector<uint8_t> b(n * 32);
+  download<F>(c, ZK_REPR_CANONICAL, dev, n, reinterpret_cast<zk_fe*>(b.data()));
+  return b;
+}
+
+inline bool pow2_ok(uint32_t nvars) { return nvars < 40; }
+
+template <class F>
+void emit_gkr(zk_repr repr, const GkrOut& g, uint32_t n, zk_fe* out_coeffs, uint8_t* out_ncoeffs,
+              zk_fe* out_challenges) {
+  for (uint32_t k = 0; k < n; ++k) {
+    out_ncoeffs[k] = g.ncoeffs[k];
+    for (int i = 0; i < 3; ++i) out_coeffs[3 * k + i] = out_repr<F>(repr, g.coeffs[3 * k + i]);
+    out_challenges[k] = out_repr<F>(repr, g.challenges[k]);
+  }
+}
+}  // namespace zkh
+using namespace zkh;

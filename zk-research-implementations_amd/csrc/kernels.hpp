@@ -349,7 +349,7 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk) {
 }
 
 // copy n u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
-__global__ void k_publish(const uint64_t* __restrict__ src, int n, uint64_t* host_out, uint32_t* host_flag,
+static __global__ void k_publish(const uint64_t* __restrict__ src, int n, uint64_t* host_out, uint32_t* host_flag,
                           uint32_t tag) {
   if (threadIdx.x < n)
     __hip_atomic_store(host_out + threadIdx.x, src[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1,0 +1,378 @@
+// Multilinear KZG over BLS12-381 G1: host driver and C ABI.
+#include "host.hpp"
+#include "msm.hpp"
+
+using namespace zkh;
+
+// a KZG setup: the Lagrange basis over the last v taus for v = 0..nv, affine
+// Montgomery on the device (bases[nv] is get_lagrange_basis's output)
+struct zk_kzg {
+  uint32_t nv = 0;
+  int device = 0;
+  std::vector<DevBuf> bases;
+  ~zk_kzg() {
+    for (auto& b : bases) b.release();
+  }
+};
+
+
+namespace {
+// ---------------------------------------------------------------------------
+// KZG over BLS12-381 G1 (pcs/src/kzg_pcs/kzg.rs). Kernels in
+// msm.hpp. Scalars are BLS12-381 Fr (the field the reference's KZG is used
+// with, gkr_protocol.rs:360); points cross the ABI as canonical affine (x, y)
+// of 48-byte LE coordinates, (0, 0) for the point at infinity.
+// ---------------------------------------------------------------------------
+using zk::Fq;
+using zk::G1A;
+using zk::G1J;
+using Fr381 = zk::Bls12_381Fr;
+
+template <class T>
+T* dptr(DevBuf& b) {
+  return reinterpret_cast<T*>(b.p);
+}
+
+// exclusive scan of n u32 in place
+void scan_u32(zk_ctx* c, uint32_t* a, uint64_t n, int depth = 0) {
+  const uint64_t nb = (n + zk::kScanBlock - 1) / zk::kScanBlock;
+  if (nb <= 1) {
+    launch(c, ZK_K_MSM, 8.0 * n, 0, zk::k_scan_block, 1u, a, n, (uint32_t*)nullptr);
+    return;
+  }
+  require(depth < 4, "scan too large");
+  DevBuf& sums = c->scan_tmp[depth];
+  sums.ensure(nb * 4);
+  launch(c, ZK_K_MSM, 8.0 * n, 0, zk::k_scan_block, (uint32_t)nb, a, n, dptr<uint32_t>(sums));
+  scan_u32(c, dptr<uint32_t>(sums), nb, depth + 1);
+  launch(c, ZK_K_MSM, 8.0 * n, 0, zk::k_scan_add, (uint32_t)((n + zk::kBlock - 1) / zk::kBlock), a, n,
+         (const uint32_t*)dptr<uint32_t>(sums));
+}
+
+uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + zk::kBlock - 1) / zk::kBlock); }
+
+// Sum each segment s = items [off[s], off[s+1]) (device u32 offsets, nseg + 1).
+// Level 0 reads affine bases[order[j]] (order != null) or Jacobian items0[j].
+// Uses c->msm[pool .. pool+4]; returns a device pointer to nseg sums.
+G1J* seg_reduce(zk_ctx* c, const G1A* bases, const uint32_t* order, const G1J* items0, const uint32_t* off,
+                uint64_t nseg, int pool) {
+  const G1J* items = items0;
+  bool gather = order != nullptr;
+  const uint32_t* cur_off = off;
+  int flip = 0;
+  for (int level = 0;; ++level) {
+    require(level < 12, "segmented reduction did not converge");
+    DevBuf& toff = c->msm[pool + flip];
+    DevBuf& tseg = c->msm[pool + 2];
+    DevBuf& part = c->msm[pool + 3 + flip];
+    toff.ensure((nseg + 1) * 4);
+    uint32_t* to = dptr<uint32_t>(toff);
+    launch(c, ZK_K_MSM, 12.0 * nseg, 0, zk::k_seg_task_counts, blocks_for(nseg), cur_off, nseg, to);
+    HIPCK(hipMemsetAsync(to + nseg, 0, 4, c->stream));
+    scan_u32(c, to, nseg + 1);
+    uint32_t total = 0;
+    HIPCK(hipMemcpyAsync(&total, to + nseg, 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    tseg.ensure((size_t)total * 4);
+    launch(c, ZK_K_MSM, 4.0 * total, 0, zk::k_seg_task_owner, blocks_for(nseg), (const uint32_t*)to, nseg, total,
+           dptr<uint32_t>(tseg));
+    part.ensure((size_t)total * sizeof(G1J));
+    if (gather)
+      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<true>, blocks_for(total), bases, order, (const G1J*)nullptr, cur_off,
+             (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg), total, dptr<G1J>(part));
+    else
+      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<false>, blocks_for(total), (const G1A*)nullptr,
+             (const uint32_t*)nullptr, items, cur_off, (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg),
+             total, dptr<G1J>(part));
+    if (total == nseg) return dptr<G1J>(part);
+    items = dptr<G1J>(part);
+    cur_off = to;
+    gather = false;
+    flip ^= 1;
+  }
+}
+
+// sum_i scalars[i] * bases[i]; scalars canonical Fr (device), bases affine Montgomery (device)
+G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
+  using namespace zk;
+  if (n == 0) return g1_inf();
+  require(n < (1ull << 28), "MSM too large");
+  uint32_t lg = 0;
+  while ((2ull << lg) <= n) ++lg;
+  const uint32_t cb = std::min<uint32_t>(20, std::max<uint32_t>(5, lg > 8 ? lg - 3 : 5));
+  const uint32_t W = (255 + cb - 1) / cb;
+  const uint64_t nb = (uint64_t)W << cb;
+  DevBuf& cnt = c->msm[10];
+  DevBuf& cur = c->msm[11];
+  DevBuf& ord = c->msm[12];
+  cnt.ensure((nb + 1) * 4);
+  cur.ensure(nb * 4);
+  ord.ensure(std::max<uint64_t>(1, n * W) * 4);
+  HIPCK(hipMemsetAsync(cnt.p, 0, (nb + 1) * 4, c->stream));
+  const uint32_t g = grid_for(c, n, k_msm_count);
+  launch(c, ZK_K_MSM, 32.0 * n, 0, k_msm_count, g, scalars, n, cb, W, dptr<uint32_t>(cnt));
+  scan_u32(c, dptr<uint32_t>(cnt), nb + 1);
+  HIPCK(hipMemcpyAsync(cur.p, cnt.p, nb * 4, hipMemcpyDeviceToDevice, c->stream));
+  launch(c, ZK_K_MSM, 32.0 * n, 0, k_msm_scatter, g, scalars, n, cb, W, dptr<uint32_t>(cur), dptr<uint32_t>(ord));
+  // bucket sums (mixed additions of the gathered affine bases)
+  G1J* buckets = seg_reduce(c, bases, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
+  // per window: sum_d d B_d over chunks of buckets, then over the chunks
+  const uint32_t chunks = (1u << cb) / kBucketChunk;
+  DevBuf& chb = c->msm[13];
+  chb.ensure((size_t)W * chunks * sizeof(G1J));
+  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * chunks), (const G1J*)buckets, cb, W,
+         dptr<G1J>(chb));
+  std::vector<uint32_t> woff(W + 1);
+  for (uint32_t w = 0; w <= W; ++w) woff[w] = w * chunks;
+  DevBuf& wo = c->msm[14];
+  wo.ensure((W + 1) * 4);
+  HIPCK(hipMemcpyAsync(wo.p, woff.data(), (W + 1) * 4, hipMemcpyHostToDevice, c->stream));
+  G1J* ws = seg_reduce(c, nullptr, nullptr, dptr<G1J>(chb), dptr<uint32_t>(wo), W, 5);
+  std::vector<G1J> S(W);
+  HIPCK(hipMemcpyAsync(S.data(), ws, W * sizeof(G1J), hipMemcpyDeviceToHost, c->stream));
+  sync(c);
+  // Horner over the windows on the host: R = sum_w 2^(c w) S_w
+  G1J R = S[W - 1];
+  for (uint32_t w = W - 1; w-- > 0;) {
+    for (uint32_t k = 0; k < cb; ++k) R = g1_dbl(R);
+    R = g1_add(R, S[w]);
+  }
+  return R;
+}
+
+// batch Jacobian -> affine on the host (Montgomery's trick)
+std::vector<G1A> host_normalize(const std::vector<G1J>& pts) {
+  using namespace zk;
+  std::vector<Fq> pre(pts.size());
+  Fq acc = fq_one();
+  for (size_t i = 0; i < pts.size(); ++i) {
+    pre[i] = acc;
+    if (!g1_is_inf(pts[i])) acc = fq_mul(acc, pts[i].Z);
+  }
+  Fq inv = fq_inv(acc);
+  std::vector<G1A> out(pts.size());
+  for (size_t i = pts.size(); i-- > 0;) {
+    if (g1_is_inf(pts[i])) {
+      out[i] = {fq_zero(), fq_zero()};
+      continue;
+    }
+    out[i] = g1_to_affine_zi(pts[i], fq_mul(inv, pre[i]));
+    inv = fq_mul(inv, pts[i].Z);
+  }
+  return out;
+}
+
+G1A g1_generator() {
+  Fq x, y;
+  memcpy(x.v, zk::kG1GenX, 48);
+  memcpy(y.v, zk::kG1GenY, 48);
+  return {zk::fq_to_mont(x), zk::fq_to_mont(y)};
+}
+
+// table[w * 256 + d] = d * 2^(8w) * G, affine on the device (built once per ctx)
+const G1A* g1_fixed_table(zk_ctx* c) {
+  using namespace zk;
+  if (c->g1_table.p) return dptr<G1A>(c->g1_table);
+  std::vector<G1J> t(32 * 256, g1_inf());
+  G1J gw = g1_from_affine(g1_generator());
+  for (int w = 0; w < 32; ++w) {
+    for (int d = 1; d < 256; ++d) t[w * 256 + d] = d == 1 ? gw : g1_add(t[w * 256 + d - 1], gw);
+    for (int k = 0; k < 8; ++k) gw = g1_dbl(gw);
+  }
+  const std::vector<G1A> a = host_normalize(t);
+  c->g1_table.ensure(a.size() * sizeof(G1A));
+  HIPCK(hipMemcpyAsync(c->g1_table.p, a.data(), a.size() * sizeof(G1A), hipMemcpyHostToDevice, c->stream));
+  sync(c);
+  return dptr<G1A>(c->g1_table);
+}
+
+zk_g1 g1_out(const G1J& p) {
+  const G1A a = zk::g1_to_affine(p);
+  zk_g1 r;
+  const Fq x = zk::fq_from_mont(a.x), y = zk::fq_from_mont(a.y);
+  memcpy(r.x, x.v, 48);
+  memcpy(r.y, y.v, 48);
+  return r;
+}
+zk_g1 g1a_out(const G1A& a) {
+  zk_g1 r;
+  const Fq x = zk::g1a_is_inf(a) ? zk::fq_zero() : zk::fq_from_mont(a.x);
+  const Fq y = zk::g1a_is_inf(a) ? zk::fq_zero() : zk::fq_from_mont(a.y);
+  memcpy(r.x, x.v, 48);
+  memcpy(r.y, y.v, 48);
+  return r;
+}
+
+// Fr values (host, repr) -> canonical Fr on the device (k_check_canonical + conversion)
+void upload_fr_canonical(zk_ctx* c, zk_repr repr, const zk_fe* host, uint64_t n, Fe* dev) {
+  upload<Fr381>(c, repr, host, n, dev);  // -> Montgomery, checked < r
+  launch(c, ZK_K_CONVERT, 64.0 * n, (double)n, zk::k_convert<Fr381, false>, grid_for(c, n, zk::k_convert<Fr381, false>),
+         (const Fe*)dev, dev, n);
+}
+
+G1J kzg_commit_canonical(zk_ctx* c, const zk_kzg* k, uint32_t v, const Fe* scalars) {
+  return msm_g1_device(c, reinterpret_cast<const G1A*>(k->bases[v].p), scalars, (uint64_t)1 << v);
+}
+
+// KZG::get_proof (kzg.rs:59-95): quotient i of (f - v) w.r.t. its top variable,
+// committed against the basis of the remaining variables — the same group
+// element as the reference's commitment of the blown-up quotient against the
+// full basis, since sum_k L_(k, j) over the blown-up top variables is L_j of
+// the suffix basis (eq sums to 1) — then fold f by point[i].
+void kzg_get_proof(zk_ctx* c, const zk_kzg* k, const Fe* f_mont, const Fe& v_mont, const std::vector<Fe>& point,
+                   std::vector<G1J>& out) {
+  using namespace zk;
+  const uint32_t nv = k->nv;
+  const uint64_t N = (uint64_t)1 << nv;
+  DevBuf& a = c->msm[15];
+  a.ensure(N * 32 + (N / 2 + 1) * 32 * 2);
+  Fe* cur = reinterpret_cast<Fe*>(a.p);
+  Fe* nxt = cur + N;
+  Fe* q = nxt + N / 2;
+  launch(c, ZK_K_FOLD, 64.0 * N, 0, k_sub_const<Fr381>, grid_for(c, N, k_sub_const<Fr381>), f_mont, N, v_mont, cur);
+  out.clear();
+  for (uint32_t i = 0; i < nv; ++i) {
+    const uint32_t m = nv - i;  // variables of cur
+    const uint64_t half = (uint64_t)1 << (m - 1);
+    launch(c, ZK_K_FOLD, 96.0 * half, 0, k_top_diff<Fr381>, grid_for(c, half, k_top_diff<Fr381>), (const Fe*)cur,
+           half, q);
+    launch(c, ZK_K_CONVERT, 64.0 * half, (double)half, k_convert<Fr381, false>,
+           grid_for(c, half, k_convert<Fr381, false>), (const Fe*)q, q, half);
+    out.push_back(kzg_commit_canonical(c, k, m - 1, q));
+    launch(c, ZK_K_FOLD, 96.0 * half, (double)half, k_fold<Fr381>, grid_for(c, half, k_fold<Fr381>), (const Fe*)cur,
+           nxt, half, m - 1, point[i]);
+    std::swap(cur, nxt);
+  }
+}
+}  // namespace
+
+extern "C" {
+
+// ---- KZG over BLS12-381 G1 ----
+int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_kzg** out) {
+  return guarded([&] {
+    require(c && taus && out, "null argument");
+    require(nvars >= 1, "Invalid num of vars for lagrange basis");  // kzg.rs:184-186
+    require(nvars <= 26, "KZG setup too large");
+    bind(c);
+    *out = nullptr;
+    auto k = std::make_unique<zk_kzg>();
+    k->nv = nvars;
+    k->device = c->device;
+    k->bases.resize(nvars + 1);
+    const uint64_t N = (uint64_t)1 << nvars;
+    const G1A* table = g1_fixed_table(c);
+    DevBuf& tb = c->msm[14];
+    tb.ensure(nvars * 32);
+    upload<Fr381>(c, repr, taus, nvars, reinterpret_cast<Fe*>(tb.p));
+    DevBuf& sc = c->msm[15];
+    sc.ensure(N * 32);
+    launch(c, ZK_K_MSM, 32.0 * N, (double)N * nvars, zk::k_eq_scalars<Fr381>, grid_for(c, N, zk::k_eq_scalars<Fr381>),
+           (const Fe*)tb.p, nvars, N, reinterpret_cast<Fe*>(sc.p));
+    DevBuf& jac = c->msm[13];
+    jac.ensure(N * sizeof(G1J));
+    launch(c, ZK_K_MSM, 176.0 * N, 0, zk::k_fixed_base, grid_for(c, N, zk::k_fixed_base), table,
+           (const Fe*)sc.p, N, dptr<G1J>(jac));
+    for (uint32_t v = nvars + 1; v-- > 0;) {
+      const uint64_t n = (uint64_t)1 << v;
+      if (v < nvars)
+        launch(c, ZK_K_MSM, 336.0 * n, 0, zk::k_pair_sum, grid_for(c, n, zk::k_pair_sum),
+               (const G1A*)k->bases[v + 1].p, n, dptr<G1J>(jac));
+      k->bases[v].ensure(n * sizeof(G1A));
+      launch(c, ZK_K_MSM, 240.0 * n, 0, zk::k_batch_normalize, blocks_for((n + zk::kBatchNorm - 1) / zk::kBatchNorm),
+             (const G1J*)dptr<G1J>(jac), n, dptr<G1A>(k->bases[v]));
+    }
+    sync(c);
+    *out = k.release();
+  });
+}
+
+void zk_kzg_free(zk_kzg* k) {
+  if (!k) return;
+  (void)hipSetDevice(k->device);
+  delete k;
+}
+
+int zk_kzg_lagrange_basis(zk_ctx* c, const zk_kzg* k, uint32_t nvars_suffix, zk_g1* out) {
+  return guarded([&] {
+    require(c && k && out, "null argument");
+    require(nvars_suffix <= k->nv, "no such basis");
+    bind(c);
+    const uint64_t n = (uint64_t)1 << nvars_suffix;
+    std::vector<G1A> a(n);
+    HIPCK(hipMemcpyAsync(a.data(), k->bases[nvars_suffix].p, n * sizeof(G1A), hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    for (uint64_t i = 0; i < n; ++i) out[i] = g1a_out(a[i]);
+  });
+}
+
+int zk_kzg_commit(zk_ctx* c, const zk_kzg* k, zk_repr repr, const zk_fe* evals, zk_g1* out) {
+  return guarded([&] {
+    require(c && k && evals && out, "null argument");
+    bind(c);
+    const uint64_t N = (uint64_t)1 << k->nv;
+    c->input.ensure(N * 32);
+    upload_fr_canonical(c, repr, evals, N, c->input.fe());
+    *out = g1_out(kzg_commit_canonical(c, k, k->nv, c->input.fe()));
+  });
+}
+
+int zk_dev_kzg_commit(zk_ctx* c, const zk_kzg* k, const void* dev_evals, zk_g1* out) {
+  return guarded([&] {
+    require(c && k && dev_evals && out, "null argument");
+    bind(c);
+    const uint64_t N = (uint64_t)1 << k->nv;
+    c->input.ensure(N * 32);
+    launch(c, ZK_K_CONVERT, 64.0 * N, (double)N, zk::k_convert<Fr381, false>, grid_for(c, N, zk::k_convert<Fr381, false>),
+           reinterpret_cast<const Fe*>(dev_evals), c->input.fe(), N);
+    *out = g1_out(kzg_commit_canonical(c, k, k->nv, c->input.fe()));
+  });
+}
+
+int zk_kzg_get_proof(zk_ctx* c, const zk_kzg* k, zk_repr repr, const zk_fe* evals, const zk_fe* opened_value,
+                     const zk_fe* point, zk_g1* out) {
+  return guarded([&] {
+    require(c && k && evals && opened_value && point && out, "null argument");
+    bind(c);
+    const uint64_t N = (uint64_t)1 << k->nv;
+    c->input.ensure(N * 32);
+    upload<Fr381>(c, repr, evals, N, c->input.fe());
+    std::vector<Fe> pt(k->nv);
+    for (uint32_t i = 0; i < k->nv; ++i) pt[i] = in_mont<Fr381>(repr, point[i]);
+    std::vector<G1J> q;
+    kzg_get_proof(c, k, c->input.fe(), in_mont<Fr381>(repr, *opened_value), pt, q);
+    for (uint32_t i = 0; i < k->nv; ++i) out[i] = g1_out(q[i]);
+  });
+}
+
+int zk_msm_g1(zk_ctx* c, zk_repr repr, const zk_g1* bases, const zk_fe* scalars, size_t n, zk_g1* out) {
+  return guarded([&] {
+    require(c && out && (n == 0 || (bases && scalars)), "null argument");
+    bind(c);
+    std::vector<G1A> b(n);
+    for (size_t i = 0; i < n; ++i) {
+      Fq x, y;
+      memcpy(x.v, bases[i].x, 48);
+      memcpy(y.v, bases[i].y, 48);
+      require(zk::fq_is_canonical(x) && zk::fq_is_canonical(y), "point coordinate >= modulus");
+      if (zk::fq_is_zero(x) && zk::fq_is_zero(y)) {
+        b[i] = {zk::fq_zero(), zk::fq_zero()};
+      } else {
+        b[i] = {zk::fq_to_mont(x), zk::fq_to_mont(y)};
+        const Fq lhs = zk::fq_sqr(b[i].y);
+        Fq four = zk::fq_zero();
+        four.v[0] = 4;
+        const Fq rhs = zk::fq_add(zk::fq_mul(zk::fq_sqr(b[i].x), b[i].x), zk::fq_to_mont(four));
+        require(zk::fq_eq(lhs, rhs), "point not on the curve");
+      }
+    }
+    DevBuf& db = c->msm[9];
+    db.ensure(std::max<size_t>(1, n) * sizeof(G1A));
+    if (n) HIPCK(hipMemcpyAsync(db.p, b.data(), n * sizeof(G1A), hipMemcpyHostToDevice, c->stream));
+    c->input.ensure(std::max<size_t>(1, n) * 32);
+    upload_fr_canonical(c, repr, scalars, n, c->input.fe());
+    *out = g1_out(msm_g1_device(c, dptr<G1A>(db), c->input.fe(), n));
+  });
+}
+
+}  // extern "C"
