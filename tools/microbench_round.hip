@@ -61,8 +61,11 @@ __global__ __launch_bounds__(kBlock) void k_round(const Fe* __restrict__ A, cons
 }
 
 // round 0 body (k_gkr_round0: 2 threads per pair, 4 loads, 3 unreduced products)
+#ifndef R0_WAVES
+#define R0_WAVES 1
+#endif
 template <class F, int MODE>  // 0 real, 1 compute-only, 2 memory-only
-__global__ __launch_bounds__(kBlock) void k_round0(const Fe* __restrict__ A, const Fe* __restrict__ S,
+__global__ __launch_bounds__(kBlock, R0_WAVES) void k_round0(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                    const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t h,
                                                    Fe* out) {
   Wide w0 = wide_zero<F>(), w1 = wide_zero<F>(), w2 = wide_zero<F>();

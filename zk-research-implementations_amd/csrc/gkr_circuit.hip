@@ -75,7 +75,7 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
   vals.b.ensure(nvals * 32);
   dops.b.ensure(opoff[nlayers]);
   dwt.b.ensure((size_t)gates[0] * 32);
-  dpts.b.ensure(64 * 32);
+  dpts.b.ensure(64 * 32);  // challenge points (<= 2 x 14)
   upload<F>(c, repr, inputs, ninputs, vals.b.fe(0));
   HIPCK(hipMemcpyAsync(dops.b.p, ops, opoff[nlayers], hipMemcpyHostToDevice, c->stream));
   const uint8_t* dop = reinterpret_cast<const uint8_t*>(dops.b.p);
@@ -142,7 +142,16 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     k0 += nv;
     rb.assign(g.challenges.begin(), g.challenges.begin() + nv / 2);  // (:71-73)
     rc.assign(g.challenges.begin() + nv / 2, g.challenges.end());
-    const Fe o1 = mle_evaluate_device<F>(c, w, lgL, rb), o2 = mle_evaluate_device<F>(c, w, lgL, rc);  // (:75-76)
+    // o1 = w.evaluate(r_b), o2 = w.evaluate(r_c) (:75-76): one fused pass
+    std::vector<Fe> rbc(rb);
+    rbc.insert(rbc.end(), rc.begin(), rc.end());
+    HIPCK(hipMemcpyAsync(dpts.b.p, rbc.data(), rbc.size() * 32, hipMemcpyHostToDevice, c->stream));
+    const zk::RoundSink sk = make_sink(c, false);
+    launch(c, ZK_K_LAYER, 32.0 * (2 * G), 4.0 * (2 * G), k_mle_eval2<F>, grid_for(c, 2 * (uint64_t)G, k_mle_eval2<F>), w,
+           lgL, dpts.b.fe(0), sk);
+    Fe ev[2];
+    collect_sums<F, 2>(c, sk, false, 17, ev);
+    const Fe o1 = ev[0], o2 = ev[1];
     if (idx + 1 < nlayers) {  // (:80-89)
       absorb<F>(&tr, &o1, 1);
       alpha = challenge<F>(&tr);

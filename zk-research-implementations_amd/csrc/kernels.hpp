@@ -684,6 +684,48 @@ __global__ __launch_bounds__(kBlock) void k_layer_tables(const Fe* __restrict__ 
   }
 }
 
+// Both evaluations w.evaluate(r_b), w.evaluate(r_c) of a layer's input table
+// (gkr_protocol.rs:75-76) in one pass. evaluate folds variable 0 (the MSB)
+// first, so w(r) = sum_j w[j] eq(r, j) with eq MSB-first; eq splits into the
+// top and bottom halves of the index bits, eq(r, j) = E_hi[j_hi] E_lo[j_lo].
+// Every block builds the four half tables in LDS, each thread accumulates
+// w[j] E_hi E_lo unreduced, and the two sums leave through the integer
+// epilogue (K = 2 product sums of 17 limbs). n <= 14.
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_mle_eval2(const Fe* __restrict__ w, uint32_t n,
+                                                      const Fe* __restrict__ pts /* r_b[n], r_c[n] */,
+                                                      RoundSink sink) {
+  constexpr uint32_t kHalf = 128;
+  __shared__ Fe tab[4][kHalf];  // r_b hi, r_b lo, r_c hi, r_c lo
+  const uint32_t nl = n / 2, nhi = n - nl;
+  const Fe one = fe_one<F>();
+  for (uint32_t t = threadIdx.x; t < 4 * kHalf; t += kBlock) {
+    const uint32_t which = t / kHalf, x = t % kHalf, hi = (which & 1u) == 0;
+    const uint32_t bits = hi ? nhi : nl, off = (which >> 1) * n + (hi ? 0 : nhi);
+    if (x >= (1u << bits)) continue;
+    Fe e = one;
+    for (uint32_t k = 0; k < bits; ++k) {
+      const Fe rk = ld_fe(pts, off + k);
+      e = fe_mul<F>(e, ((x >> (bits - 1 - k)) & 1u) ? rk : fe_sub<F>(one, rk));
+    }
+    tab[which][x] = e;
+  }
+  __syncthreads();
+  Wide a0 = wide_zero<F>(), a1 = wide_zero<F>();
+  const uint64_t N = (uint64_t)1 << n, stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < N; j += stride) {
+    const uint32_t x = (uint32_t)(j >> nl), y = (uint32_t)(j & ((1u << nl) - 1u));
+    const Fe wj = ld_fe(w, j);
+    wide_mac<F>(a0, fe_mul<F>(wj, tab[0][x]), tab[1][y]);
+    wide_mac<F>(a1, fe_mul<F>(wj, tab[2][x]), tab[3][y]);
+  }
+  __shared__ LimbScratch<17> sc;
+  block_limb_sums(a0, sc, 0);
+  block_limb_sums(a1, sc, 17);
+  __syncthreads();
+  grid_finish<34>(sc, sink);
+}
+
 // one circuit layer (gkr_circuit.rs:127-143): out[g] = in[2g] op in[2g+1]
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_circuit_layer(const Fe* __restrict__ in, const uint8_t* __restrict__ ops,
