@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-sample-nvars", type=int, default=22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-tables (PCIe-inclusive) prove")
+    ap.add_argument("--cpu-fast-nvars", type=int, default=24, help="size of the OpenMP CPU restatement run")
     ap.add_argument("--no-circuit", action="store_true", help="skip the full GKR circuit prove (SURVEY 8(f2))")
     ap.add_argument("--no-config5", action="store_true", help="skip BLS12-381 GKR + KZG commit (BASELINE config 5)")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
@@ -55,7 +57,7 @@ def cpu_model() -> str:
     return platform.processor()
 
 
-def cpu_baseline(field: int, nvars: int) -> dict:
+def cpu_baseline(field: int, nvars: int, fast_nvars: int) -> dict:
     """Reference CPU path: the C restatement of the reference prover
     (oracle/zk_oracle.c, same algorithm and allocation pattern as
     sum_check_protocol.rs:86-166), single thread like the reference (no rayon),
@@ -68,6 +70,15 @@ def cpu_baseline(field: int, nvars: int) -> dict:
     co.gkr_prove(field, tabs, co.Transcript())
     dt = time.perf_counter() - t0
     ops = 32.0 * ((1 << nvars) - 1)
+    del tabs
+    # the fast restatement (fused, in place, OpenMP on every thread this
+    # process may use) on the full workload: the best the host can do
+    nf = fast_nvars
+    ftabs = [co.synth(field, 3, t, 0, 1 << nf) for t in range(4)]
+    t0 = time.perf_counter()
+    co.gkr_prove(field, ftabs, co.Transcript(), fast=True)
+    dtf = time.perf_counter() - t0
+    del ftabs
     return {
         "value": ops / dt,
         "unit": "field-ops/s",
@@ -76,6 +87,14 @@ def cpu_baseline(field: int, nvars: int) -> dict:
         "sample": f"one gkr_prove over a {nvars}-var synthetic SumPoly (4 tables x 2^{nvars}), "
         f"{dt:.2f} s single-thread, host '{cpu_model()}' ({os.cpu_count()} logical CPUs)",
         "prover_ms_sample": dt * 1e3,
+        "fast_allcores": {
+            "value": 32.0 * ((1 << nf) - 1) / dtf,
+            "unit": "field-ops/s",
+            "cores": co.threads(),
+            "kind": "port (fused OpenMP restatement, oracle/zk_oracle.c or_gkr_prove_fast)",
+            "sample": f"one gkr_prove over {nf} vars (4 tables x 2^{nf}, same seed as the GPU run)",
+            "prover_ms": dtf * 1e3,
+        },
     }
 
 
@@ -109,6 +128,47 @@ def fold_bench(ctx, field: int, nvars: int = 20, reps: int = 10) -> dict:
         "bytes_per_launch": k["alg_bytes"] / k["launches"],
         "achieved_GBs": gbs,
         "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
+    }
+
+
+def e2e_bench(ctx, field: int, tabs, n: int, reps: int = 3) -> dict:
+    """The PCIe-inclusive rate (SURVEY.md 8(d) "end-to-end time including
+    H2D"), never `value`: the same proof through the host-pointer ABI
+    zk_gkr_sumcheck_prove, tables handed over in host memory in ark's
+    Montgomery layout (what a Rust shim passes without conversion), uploaded by
+    the library inside the call. Host buffers are ordinary pageable memory."""
+    import ctypes as C
+
+    import numpy as np
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+    from zk_amd.context import REPR_MONTGOMERY
+    from zk_amd.elems import as_limbs, ptr
+
+    host = [t.download(REPR_MONTGOMERY) for t in tabs]
+    arr = (C.c_void_p * 4)(*[h.ctypes.data for h in host])
+    coeffs = np.zeros((n, 3, 4), np.uint64)
+    nco = np.zeros(n, np.uint8)
+    ch = np.zeros((n, 4), np.uint64)
+    cs = np.zeros((1, 4), np.uint64)
+    zero = as_limbs([0])
+    times = []
+    for i in range(reps + 1):
+        tr = zk_amd.Transcript(field)
+        t0 = time.perf_counter()
+        check(lib().zk_gkr_sumcheck_prove(ctx.h, field, REPR_MONTGOMERY, arr, n, ptr(zero), tr.h, ptr(coeffs),
+                                          ptr(nco), ptr(ch), ptr(cs)))
+        if i:
+            times.append(time.perf_counter() - t0)
+    times.sort()
+    gib = 4 * (1 << n) * 32
+    return {
+        "workload": f"zk_gkr_sumcheck_prove from host memory, {n} vars, 4 tables x 2^{n} ({gib / 2**30:.0f} GiB)",
+        "ms_median": times[len(times) // 2] * 1e3,
+        "upload_GBs_effective": gib / times[len(times) // 2] / 1e9,
+        # outputs follow the input repr (Montgomery); canonical for the caller's comparison
+        "challenges": ctx.upload(field, ch, REPR_MONTGOMERY).download(),
     }
 
 
@@ -357,6 +417,10 @@ def main() -> None:
                 "launches_by_kind": {kk: v["launches"] / args.steps for kk, v in k.items() if v["launches"]},
             },
         }
+        if not args.no_e2e and world == 1:
+            e2e = e2e_bench(ctx, field, tabs, n)
+            e2e["same_proof_as_device_resident"] = bool(np.array_equal(e2e.pop("challenges"), ch))
+            out["e2e_host_tables"] = e2e
         if not args.no_fold and world == 1:
             out["fold_20var"] = fold_bench(ctx, field)
         if not args.no_circuit and world == 1:
@@ -364,7 +428,7 @@ def main() -> None:
         if not args.no_config5 and world == 1:
             out["config5_bls12_381"] = config5_bench(ctx)
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(field, args.cpu_sample_nvars)
+            cb = cpu_baseline(field, args.cpu_sample_nvars, args.cpu_fast_nvars)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = value / cb["value"]
         print(json.dumps(out), flush=True)

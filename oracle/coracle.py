@@ -43,6 +43,8 @@ def lib():
         L.or_sumcheck_prove.argtypes = [i32, P, u32, P, P]
         L.or_sumcheck_verify.argtypes = [i32, P, u32, P, u32, u32, P]
         L.or_gkr_prove.argtypes = [i32, P, u32, P, P, P, P]
+        L.or_gkr_prove_fast.argtypes = [i32, P, u32, P, P, P, P]
+        L.or_threads.restype = i32
         L.or_gkr_verify.argtypes = [i32, P, P, u32, P, P, P, P]
         L.or_synth_fill.argtypes = [i32, u64, u32, u64, u64, P]
         L.or_fe_from_le_bytes_mod_order.argtypes = [i32, P, C.c_size_t, P]
@@ -146,14 +148,21 @@ def verify(field: int, evals: np.ndarray, round_polys: np.ndarray, claimed: int)
     return lib().or_sumcheck_verify(field, _ptr(evals), n, _ptr(buf), nrounds, plen, _ptr(to_limbs([claimed])))
 
 
-def gkr_prove(field: int, tables, transcript: Transcript):
+def threads() -> int:
+    return int(lib().or_threads())
+
+
+def gkr_prove(field: int, tables, transcript: Transcript, fast: bool = False):
+    """or_gkr_prove (reference-faithful, 1 thread) or, with fast=True,
+    or_gkr_prove_fast (fused, in place, OpenMP; identical outputs)."""
     tabs = [np.ascontiguousarray(t, dtype=np.uint64) for t in tables]
     n = tabs[0].shape[0].bit_length() - 1
     arr = (C.c_void_p * 4)(*[t.ctypes.data for t in tabs])
     coeffs = np.zeros((max(n, 1), 3, 4), np.uint64)
     nco = np.zeros(max(n, 1), np.uint8)
     ch = np.zeros((max(n, 1), 4), np.uint64)
-    assert lib().or_gkr_prove(field, arr, n, transcript.h, _ptr(coeffs), _ptr(nco), _ptr(ch)) == 0
+    fn = lib().or_gkr_prove_fast if fast else lib().or_gkr_prove
+    assert fn(field, arr, n, transcript.h, _ptr(coeffs), _ptr(nco), _ptr(ch)) == 0
     polys = [from_limbs(coeffs[k, : nco[k]]) for k in range(n)]
     return polys, from_limbs(ch[:n])
 

@@ -8,6 +8,9 @@
 
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 typedef unsigned __int128 u128;
 
@@ -647,6 +650,75 @@ int or_gkr_prove(int field, const or_fe* const tables[4], uint32_t nvars, or_tra
   }
   sp_free(&cur);
   return 0;
+}
+
+/* The fast CPU restatement ("also report the fast OpenMP
+ * restatement on all cores"): the same transcript as or_gkr_prove, without the
+ * reference's per-round copies. Per round one parallel pass computes the three
+ * evaluations e_t = sum_j A_t S_t + M_t P_t (X_t = X_lo + t (X_hi - X_lo)),
+ * the round polynomial is interpolated and trimmed exactly as above, and a
+ * second pass folds the four tables in place: 10 Montgomery muls per pair. */
+int or_gkr_prove_fast(int field, const or_fe* const tables[4], uint32_t nvars, or_transcript* t, or_fe* out_coeffs,
+                      uint8_t* out_ncoeffs, or_fe* out_challenges) {
+  const or_params* P = params(field);
+  if (!P) return -1;
+  const size_t N = (size_t)1 << nvars;
+  mfe* X[4];
+  for (int k = 0; k < 4; ++k) {
+    X[k] = (mfe*)malloc(N * sizeof(mfe));
+    if (!X[k]) {
+      for (int q = 0; q < k; ++q) free(X[q]);
+      return -1;
+    }
+    mfe* dst = X[k];
+    const or_fe* src = tables[k];
+#pragma omp parallel for schedule(static)
+    for (size_t i = 0; i < N; ++i) dst[i] = m_from_canon(P, &src[i]);
+  }
+  mfe xs[3];
+  for (int i = 0; i < 3; ++i) xs[i] = m_from_u64(P, (uint64_t)i);
+  size_t len = N;
+  for (uint32_t round = 0; round < nvars; ++round) {
+    const size_t h = len / 2;
+    mfe e[3] = {m_zero(), m_zero(), m_zero()};
+#pragma omp parallel
+    {
+      mfe acc[3] = {m_zero(), m_zero(), m_zero()};
+#pragma omp for schedule(static) nowait
+      for (size_t j = 0; j < h; ++j) {
+        mfe v[4][3];
+        for (int k = 0; k < 4; ++k) {
+          v[k][0] = X[k][j];
+          v[k][1] = X[k][j + h];
+          v[k][2] = m_sub(P, m_add(P, v[k][1], v[k][1]), v[k][0]);
+        }
+        for (int q = 0; q < 3; ++q)
+          acc[q] = m_add(P, acc[q], m_add(P, m_mul(P, v[0][q], v[1][q]), m_mul(P, v[2][q], v[3][q])));
+      }
+#pragma omp critical
+      for (int q = 0; q < 3; ++q) e[q] = m_add(P, e[q], acc[q]);
+    }
+    upoly rp = up_interpolate(P, xs, e, 3);
+    tr_append_fes(P, t, rp.c, (size_t)rp.n);
+    out_ncoeffs[round] = (uint8_t)rp.n;
+    for (int i = 0; i < 3; ++i) out_coeffs[3 * round + i] = m_to_canon(P, i < rp.n ? rp.c[i] : m_zero());
+    const mfe r = tr_challenge(P, t);
+    out_challenges[round] = m_to_canon(P, r);
+#pragma omp parallel for schedule(static)
+    for (size_t j = 0; j < h; ++j)
+      for (int k = 0; k < 4; ++k) X[k][j] = m_add(P, X[k][j], m_mul(P, r, m_sub(P, X[k][j + h], X[k][j])));
+    len = h;
+  }
+  for (int k = 0; k < 4; ++k) free(X[k]);
+  return 0;
+}
+
+int or_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
 }
 
 /* gkr_verify (:117-150) */

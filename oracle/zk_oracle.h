@@ -71,6 +71,10 @@ int or_sumcheck_verify(int field, const or_fe* evals, uint32_t nvars, const or_f
  * transcript is caller-owned and mutated; out_coeffs[3*nvars], out_ncoeffs[nvars], out_challenges[nvars] */
 int or_gkr_prove(int field, const or_fe* const tables[4], uint32_t nvars, or_transcript* t, or_fe* out_coeffs,
                  uint8_t* out_ncoeffs, or_fe* out_challenges);
+/* same outputs as or_gkr_prove: fused, in place, OpenMP over all threads (the fast CPU restatement) */
+int or_gkr_prove_fast(int field, const or_fe* const tables[4], uint32_t nvars, or_transcript* t, or_fe* out_coeffs,
+                      uint8_t* out_ncoeffs, or_fe* out_challenges);
+int or_threads(void); /* OpenMP threads or_gkr_prove_fast uses */
 /* gkr_verify: returns verified (1/0); out_final_claim, out_challenges[nrounds] (on failure: final 0, 1 challenge 0) */
 int or_gkr_verify(int field, const or_fe* coeffs, const uint8_t* ncoeffs, uint32_t nrounds, const or_fe* claimed_sum,
                   or_transcript* t, or_fe* out_final_claim, or_fe* out_challenges);

@@ -169,7 +169,8 @@ def test_golden_sumcheck_12(golden):
         assert [co.from_limbs(x) for x in rp] == [[h2i(a), h2i(b)] for a, b in g["round_polys"]]
 
 
-def test_golden_gkr_10(golden):
+@pytest.mark.parametrize("fast", [False, True])
+def test_golden_gkr_10(golden, fast):  # fast: the fused OpenMP restatement, same transcript
     for g in golden["gkr_prove_10"]:
         tabs = []
         for s in g["inputs"]:
@@ -177,13 +178,14 @@ def test_golden_gkr_10(golden):
             assert hashlib.sha256(tab.astype("<u8").tobytes()).hexdigest() == s["sha256"]
             tabs.append(tab)
         f = g["inputs"][0]["field"]
-        polys, chal = co.gkr_prove(f, tabs, co.Transcript())
+        polys, chal = co.gkr_prove(f, tabs, co.Transcript(), fast=fast)
         assert polys == [[h2i(c) for c in p] for p in g["round_polys"]]
         assert chal == [h2i(c) for c in g["challenges"]]
 
 
-def test_golden_gkr_ref_2var(golden):
+@pytest.mark.parametrize("fast", [False, True])
+def test_golden_gkr_ref_2var(golden, fast):
     g = golden["gkr_ref_2var"]
-    polys, chal = co.gkr_prove(g["field"], [co.to_limbs(t) for t in g["tables"]], co.Transcript())
+    polys, chal = co.gkr_prove(g["field"], [co.to_limbs(t) for t in g["tables"]], co.Transcript(), fast=fast)
     assert polys == [[h2i(c) for c in p] for p in g["round_polys"]]
     assert chal == [h2i(c) for c in g["challenges"]]

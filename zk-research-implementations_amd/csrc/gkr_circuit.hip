@@ -101,7 +101,16 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
   o.sc.ncoeffs.assign(total, 0);
   o.sc.challenges.assign(total, fe_zero<F>());
   uint32_t k0 = 0;
+  static const bool dbg = getenv("ZK_DEBUG_CIRCUIT") != nullptr;
+  using clk = std::chrono::steady_clock;
+  auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+  clk::time_point t0 = clk::now(), t1, t2;
+  if (dbg) {
+    sync(c);
+    fprintf(stderr, "[circuit] evaluate+setup %.1f us\n", us(t0, clk::now()));
+  }
   for (uint32_t idx = 0; idx < nlayers; ++idx) {
+    if (dbg) t0 = clk::now();
     const uint32_t l = nlayers - 1 - idx, G = gates[l], lgL = lg2u(2 * (uint64_t)G), nv = 2 * lgL;
     const uint64_t T = (uint64_t)1 << nv;
     const Fe* w = vals.b.fe(off[l]);  // the layer's inputs
@@ -132,8 +141,13 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     launch(c, ZK_K_LAYER, 128.0 * T, (double)T, k_layer_tables<F>, grid, w, lgL, dwt.b.fe(0), dop + opoff[l], tab,
            tab + T, tab + 2 * T, tab + 3 * T);
     const Fe* dT[4] = {tab, tab + T, tab + 2 * T, tab + 3 * T};
+    if (dbg) {
+      sync(c);
+      t1 = clk::now();
+    }
     GkrOut g;
     gkr_prove_device<F>(c, dT, nv, false, &tr, g);  // gkr_prove(claimed_sum, &fbc_poly, &mut transcript) (:68)
+    if (dbg) t2 = clk::now();
     for (uint32_t k = 0; k < nv; ++k) {
       for (int i = 0; i < 3; ++i) o.sc.coeffs[3 * (size_t)(k0 + k) + i] = g.coeffs[3 * (size_t)k + i];
       o.sc.ncoeffs[k0 + k] = g.ncoeffs[k];
@@ -152,6 +166,9 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     Fe ev[2];
     collect_sums<F, 2>(c, sk, false, 17, ev);
     const Fe o1 = ev[0], o2 = ev[1];
+    if (dbg)
+      fprintf(stderr, "[circuit] layer %u nv %u: tables %.1f us, sum-check %.1f us (%.1f/round), evals %.1f us\n", idx,
+              nv, us(t0, t1), us(t1, t2), us(t1, t2) / nv, us(t2, clk::now()));
     if (idx + 1 < nlayers) {  // (:80-89)
       absorb<F>(&tr, &o1, 1);
       alpha = challenge<F>(&tr);

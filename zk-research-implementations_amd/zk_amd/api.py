@@ -76,9 +76,12 @@ class Transcript:
             raise MemoryError("zk_transcript_new failed")
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().zk_transcript_free(self.h)
-            self.h = None
+        try:
+            if getattr(self, "h", None):
+                lib().zk_transcript_free(self.h)
+                self.h = None
+        except Exception:  # interpreter shutdown: module globals may already be gone
+            pass
 
     def append(self, preimage: bytes) -> None:
         b = bytes(preimage)
