@@ -63,7 +63,7 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
   struct Scoped {
     DevBuf b;
     ~Scoped() { b.release(); }
-  } vals, dops, dwt, dpts;
+  } vals, dops, dwt;
   std::vector<size_t> off(nlayers + 1), opoff(nlayers + 1);
   off[0] = 0;
   opoff[0] = 0;
@@ -75,7 +75,6 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
   vals.b.ensure(nvals * 32);
   dops.b.ensure(opoff[nlayers]);
   dwt.b.ensure((size_t)gates[0] * 32);
-  dpts.b.ensure(64 * 32);  // challenge points (<= 2 x 14)
   upload<F>(c, repr, inputs, ninputs, vals.b.fe(0));
   HIPCK(hipMemcpyAsync(dops.b.p, ops, opoff[nlayers], hipMemcpyHostToDevice, c->stream));
   const uint8_t* dop = reinterpret_cast<const uint8_t*>(dops.b.p);
@@ -132,9 +131,10 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
       b = beta;
       has_c = 1;
     }
-    HIPCK(hipMemcpyAsync(dpts.b.p, pts.data(), pts.size() * 32, hipMemcpyHostToDevice, c->stream));
-    launch(c, ZK_K_LAYER, 32.0 * G, (double)G * (W + 2), k_gate_weights<F>, (G + kBlock - 1) / kBlock, dpts.b.fe(0),
-           dpts.b.fe(W), W, a, b, has_c, G, dwt.b.fe(0));
+    LayerPts lp{};
+    std::copy(pts.begin(), pts.end(), lp.r);
+    launch(c, ZK_K_LAYER, 32.0 * G, (double)G * (W + 2), k_gate_weights<F>, (G + kBlock - 1) / kBlock, lp, W, a, b,
+           has_c, G, dwt.b.fe(0));
     c->input.ensure(4 * T * 32);
     Fe* tab = c->input.fe();
     const uint32_t grid = grid_for(c, T, k_layer_tables<F>);
@@ -157,12 +157,12 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     rb.assign(g.challenges.begin(), g.challenges.begin() + nv / 2);  // (:71-73)
     rc.assign(g.challenges.begin() + nv / 2, g.challenges.end());
     // o1 = w.evaluate(r_b), o2 = w.evaluate(r_c) (:75-76): one fused pass
-    std::vector<Fe> rbc(rb);
-    rbc.insert(rbc.end(), rc.begin(), rc.end());
-    HIPCK(hipMemcpyAsync(dpts.b.p, rbc.data(), rbc.size() * 32, hipMemcpyHostToDevice, c->stream));
+    LayerPts ep{};
+    std::copy(rb.begin(), rb.end(), ep.r);
+    std::copy(rc.begin(), rc.end(), ep.r + lgL);
     const zk::RoundSink sk = make_sink(c, false);
     launch(c, ZK_K_LAYER, 32.0 * (2 * G), 4.0 * (2 * G), k_mle_eval2<F>, grid_for(c, 2 * (uint64_t)G, k_mle_eval2<F>), w,
-           lgL, dpts.b.fe(0), sk);
+           lgL, ep, sk);
     Fe ev[2];
     collect_sums<F, 2>(c, sk, false, 17, ev);
     const Fe o1 = ev[0], o2 = ev[1];

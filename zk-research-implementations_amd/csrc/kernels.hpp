@@ -639,10 +639,16 @@ __global__ __launch_bounds__(kBlock) void k_synth(Fe* Y, uint64_t n, uint64_t ke
 // writes all four sum-check tables: A (add wiring), S = w_b + w_c, M (mul
 // wiring), P = w_b * w_c at t = i L + j (tensor_add_mul_polynomials order).
 // ---------------------------------------------------------------------------
+// challenge points passed by value (kernel arguments): no host->device copy
+struct LayerPts {
+  Fe r[28];  // r_b then r_c, each <= 14 coordinates
+};
+
 template <class F>
-__global__ __launch_bounds__(kBlock) void k_gate_weights(const Fe* __restrict__ rb, const Fe* __restrict__ rc,
-                                                         uint32_t W, Fe alpha, Fe beta, uint32_t has_c, uint32_t G,
-                                                         Fe* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void k_gate_weights(const LayerPts pts, uint32_t W, Fe alpha, Fe beta,
+                                                         uint32_t has_c, uint32_t G, Fe* __restrict__ out) {
+  const Fe* rb = pts.r;
+  const Fe* rc = pts.r + W;
   const uint32_t idx = blockIdx.x * kBlock + threadIdx.x;
   if (idx >= G) return;
   const Fe one = fe_one<F>();
@@ -693,10 +699,13 @@ __global__ __launch_bounds__(kBlock) void k_layer_tables(const Fe* __restrict__ 
 // epilogue (K = 2 product sums of 17 limbs). n <= 14.
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_mle_eval2(const Fe* __restrict__ w, uint32_t n,
-                                                      const Fe* __restrict__ pts /* r_b[n], r_c[n] */,
-                                                      RoundSink sink) {
+                                                      const LayerPts pr /* r_b[n], r_c[n] */, RoundSink sink) {
   constexpr uint32_t kHalf = 128;
   __shared__ Fe tab[4][kHalf];  // r_b hi, r_b lo, r_c hi, r_c lo
+  __shared__ Fe pts[28];
+  if (threadIdx.x == 0)
+    for (uint32_t k = 0; k < 2 * n; ++k) pts[k] = pr.r[k];  // uniform index: scalar loads of the arguments
+  __syncthreads();
   const uint32_t nl = n / 2, nhi = n - nl;
   const Fe one = fe_one<F>();
   for (uint32_t t = threadIdx.x; t < 4 * kHalf; t += kBlock) {
@@ -705,7 +714,7 @@ __global__ __launch_bounds__(kBlock) void k_mle_eval2(const Fe* __restrict__ w, 
     if (x >= (1u << bits)) continue;
     Fe e = one;
     for (uint32_t k = 0; k < bits; ++k) {
-      const Fe rk = ld_fe(pts, off + k);
+      const Fe rk = pts[off + k];
       e = fe_mul<F>(e, ((x >> (bits - 1 - k)) & 1u) ? rk : fe_sub<F>(one, rk));
     }
     tab[which][x] = e;

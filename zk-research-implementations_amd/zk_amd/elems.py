@@ -17,21 +17,16 @@ def as_limbs(values) -> np.ndarray:
         if a.ndim != 2 or a.shape[1] != 4:
             raise ValueError("expected a uint64 array of shape [n, 4]")
         return a
-    vals = [int(v) for v in values]
-    out = np.empty((len(vals), 4), dtype=np.uint64)
-    for i, v in enumerate(vals):
-        if v < 0:
-            raise ValueError("field elements are non-negative canonical integers")
-        out[i, 0] = v & MASK64
-        out[i, 1] = (v >> 64) & MASK64
-        out[i, 2] = (v >> 128) & MASK64
-        out[i, 3] = (v >> 192) & MASK64
-    return out
+    try:
+        buf = b"".join(int(v).to_bytes(32, "little") for v in values)
+    except OverflowError:
+        raise ValueError("field elements are non-negative canonical integers below 2^256") from None
+    return np.frombuffer(bytearray(buf), dtype="<u8").reshape(-1, 4)
 
 
 def to_ints(a: np.ndarray) -> list[int]:
-    a = np.asarray(a, dtype=np.uint64).reshape(-1, 4)
-    return [int(r[0]) | int(r[1]) << 64 | int(r[2]) << 128 | int(r[3]) << 192 for r in a]
+    b = np.ascontiguousarray(a, dtype="<u8").reshape(-1, 4).tobytes()
+    return [int.from_bytes(b[i: i + 32], "little") for i in range(0, len(b), 32)]
 
 
 def one(v: int) -> np.ndarray:
