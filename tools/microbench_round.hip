@@ -13,8 +13,8 @@
 using namespace zk;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
-template <class F, int MODE>  // 0 real, 1 compute-only, 2 memory-only
-__global__ __launch_bounds__(kBlock) void k_round(const Fe* __restrict__ A, const Fe* __restrict__ S,
+template <class F, int MODE, int WAVES = 1>  // 0 real, 1 compute-only, 2 memory-only; WAVES: min waves/SIMD
+__global__ __launch_bounds__(kBlock, WAVES) void k_round(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                   const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                   Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
                                                   Fe* __restrict__ P2, uint64_t h, Fe r, Fe* out) {
@@ -149,6 +149,31 @@ int main() {
   run("real", k_round<F, 0>);
   run("compute", k_round<F, 1>);
   run("memory", k_round<F, 2>);
+  // occupancy sweep: the grid follows each variant's own occupancy
+  auto runw = [&](const char* name, auto kern) {
+    int pcu = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pcu, kern, kBlock, 0));
+    const int gw = prop.multiProcessorCount * pcu;
+    kern<<<gw, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, h, r, out);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 5; ++i) kern<<<gw, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, h, r, out);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / 5;
+    printf("%-12s %8.1f us   %7.1f GB/s (grid %d = %d/CU)\n", name, us, 768.0 * h / (us * 1e-6) / 1e9, gw, pcu);
+    return 0;
+  };
+  runw("real w2", k_round<F, 0, 2>);
+  runw("real w3", k_round<F, 0, 3>);
+  runw("real w4", k_round<F, 0, 4>);
+  runw("memory w2", k_round<F, 2, 2>);
+  runw("memory w3", k_round<F, 2, 3>);
+  runw("memory w4", k_round<F, 2, 4>);
+  runw("memory w6", k_round<F, 2, 6>);
+  runw("memory w8", k_round<F, 2, 8>);
 
   // the production kernels across round sizes, with the full epilogue
   // (two-level fan-in + publish to pinned host memory); back-to-back launches
@@ -167,14 +192,15 @@ int main() {
   const char* names[2] = {"round", "lanes"};
   for (int lg = 22; lg >= 0; lg -= 1) {
     const uint64_t hh = 1ull << lg;
-    for (int lanes = 0; lanes < 2; ++lanes) {
-      if (lanes == 1 && lg > 17) continue;
-      const uint64_t work = (lanes == 1 ? 8 : 2) * hh;
+    for (int v = 0; v < 2; ++v) {
+      if (v == 1 && lg > 17) continue;
+      const int lanes = v == 1;
+      const uint64_t work = (lanes ? 8 : 2) * hh;
       uint64_t g = (work + kBlock - 1) / kBlock;
       const uint64_t cap = (uint64_t)prop.multiProcessorCount * pc[lanes];
       if (g > cap) g = cap;
       auto launch = [&] {
-        if (lanes == 1)
+        if (v == 1)
           k_gkr_round_lanes<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, rin, sk);
         else
           k_gkr_round<F><<<(uint32_t)g, kBlock>>>(A, S, M, P, W, W + N / 2, W + N, W + 3 * N / 2, hh, rin, sk);
@@ -189,7 +215,7 @@ int main() {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       const double us = ms * 1e3 / reps;
-      printf("  pairs 2^%-2d %-6s grid %6llu  %9.2f us  %8.1f GB/s\n", lg, names[lanes],
+      printf("  pairs 2^%-2d %-6s grid %6llu  %9.2f us  %8.1f GB/s\n", lg, names[v],
              (unsigned long long)g, us, 768.0 * hh / (us * 1e-6) / 1e9);
     }
   }
