@@ -182,8 +182,8 @@ int zk_gkr_circuit_verify(zk_field field, zk_repr repr, uint32_t nlayers, const 
  *   zk_kzg_setup       KZG::new / run_trusted_setup's G1 half (:18-49): the
  *                      Lagrange basis eq(taus, i) * G for every i (MSB-first
  *                      hypercube, generate_bhc :171-181), plus the bases over
- *                      every suffix of taus used by get_proof. The G2 taus
- *                      (for the pairing-based KZG::verify) are not built.
+ *                      every suffix of taus used by get_proof, and (host)
+ *                      the G2 taus tau_i * G2 used by KZG::verify (below).
  *   zk_kzg_commit      KZG::commit (:51-53) = sum_i evals[i] * L_i (Pippenger MSM)
  *   zk_kzg_get_proof   KZG::get_proof (:59-95): nvars quotient commitments
  *   zk_kzg_lagrange_basis  the basis over the last nvars_suffix taus
@@ -203,6 +203,30 @@ int zk_dev_kzg_commit(zk_ctx* ctx, const zk_kzg* kzg, const void* dev_evals /* M
 int zk_kzg_get_proof(zk_ctx* ctx, const zk_kzg* kzg, zk_repr repr, const zk_fe* evals, const zk_fe* opened_value,
                      const zk_fe* point /* nvars */, zk_g1* out /* nvars */);
 int zk_msm_g1(zk_ctx* ctx, zk_repr repr, const zk_g1* bases, const zk_fe* scalars, size_t n, zk_g1* out);
+
+/* Verifier half (host, O(nvars) pairings; pcs/src/kzg_pcs/kzg.rs:35-49, :97-129).
+ * G2 points are affine over Fq2 = Fq[u]/(u^2+1): x = x[0] + x[1] u, canonical
+ * 48-byte LE coordinates, all zero = infinity; inputs are checked on the twist
+ * y^2 = x^3 + 4(1+u).
+ *   zk_kzg_g2_taus     KZG::g2_taus (pub field): tau_i * G2, nvars points
+ *   zk_kzg_verify      KZG::verify: 1 / 0 in *out_verified; nproof != npoint is
+ *                      ZK_EINVAL (the panic at :104-106); g2_taus holds npoint points
+ *   zk_g2_mul_generator  scalars[i] * G2 (G2Projective::mul_bigint)
+ *   zk_bls12_381_pairing Bls12_381::pairing(p, q) as 6 Fq2 = 72 u64: the
+ *                      Fq12 = Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - (1+u)) element
+ *                      c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2, each Fq2 as (re, im)
+ *                      canonical 6 x u64 (ark's field order)
+ *   zk_bls12_381_pairing_check  *out_ok = prod_i e(p_i, q_i) == 1 */
+typedef struct {
+  uint64_t x[2][6];
+  uint64_t y[2][6];
+} zk_g2;
+int zk_kzg_g2_taus(const zk_kzg* kzg, zk_g2* out /* nvars */);
+int zk_kzg_verify(zk_repr repr, const zk_g1* commitment, const zk_fe* opened_value, const zk_g1* proof,
+                  uint32_t nproof, const zk_fe* point, uint32_t npoint, const zk_g2* g2_taus, int* out_verified);
+int zk_g2_mul_generator(zk_repr repr, const zk_fe* scalars, size_t n, zk_g2* out);
+int zk_bls12_381_pairing(const zk_g1* p, const zk_g2* q, uint64_t out[72]);
+int zk_bls12_381_pairing_check(const zk_g1* p, const zk_g2* q, size_t n, int* out_ok);
 
 /* ---------------------------------------------------------------------------
  * Proof blob: a canonical byte form of a proof, so a proof

@@ -127,3 +127,39 @@ def test_invalid_inputs(ctx):
         msm_g1([(1, 2)], [1], ctx)
     with pytest.raises(ValueError, match="Invalid num of vars"):
         KZG([], ctx)
+
+
+def test_reference_verify_end_to_end(ctx):  # kzg.rs:402-463: setup, commit, open, get_proof on the GPU; verify
+    import pairing_oracle as pao
+
+    k = KZG([5, 2, 3], ctx)
+    evals = [0, 4, 0, 4, 0, 4, 3, 7]
+    point = [6, 4, 0]
+    assert k.g2_taus == pao.g2_taus([5, 2, 3])
+    c = k.commit(evals)
+    v = k.open(point, evals)
+    proof = k.get_proof(v, point, evals)
+    assert KZG.verify(c, v, proof, point, k.g2_taus)
+    assert not KZG.verify(c, v, [ko.G1, ko.G1, ko.G1], point, k.g2_taus)
+    k.close()
+
+
+def test_verify_random_12_var_opening(ctx):
+    rng = random.Random(12)
+    R = ko.R
+    n = 12
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    point = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    c = k.commit(evals)
+    v = k.open(point, evals)
+    assert v == po.evaluate(R, evals, point)
+    proof = k.get_proof(v, point, evals)
+    g2t = k.g2_taus
+    assert KZG.verify(c, v, proof, point, g2t)
+    assert not KZG.verify(c, (v + 1) % R, proof, point, g2t)
+    bad = list(proof)
+    bad[5] = ko.add(bad[5], ko.G1)
+    assert not KZG.verify(c, v, bad, point, g2t)
+    k.close()

@@ -1,15 +1,18 @@
 // Multilinear KZG over BLS12-381 G1: host driver and C ABI.
 #include "host.hpp"
 #include "msm.hpp"
+#include "pairing.hpp"
 
 using namespace zkh;
 
 // a KZG setup: the Lagrange basis over the last v taus for v = 0..nv, affine
-// Montgomery on the device (bases[nv] is get_lagrange_basis's output)
+// Montgomery on the device (bases[nv] is get_lagrange_basis's output), and the
+// G2 taus tau_i * G2 (run_trusted_setup :43-46) on the host, for verify
 struct zk_kzg {
   uint32_t nv = 0;
   int device = 0;
   std::vector<DevBuf> bases;
+  std::vector<zk::G2A> g2_taus;
   ~zk_kzg() {
     for (auto& b : bases) b.release();
   }
@@ -203,6 +206,61 @@ zk_g1 g1a_out(const G1A& a) {
   return r;
 }
 
+// caller point (canonical affine, (0, 0) = infinity) -> Montgomery, checked on the curve
+G1A parse_g1(const zk_g1& p) {
+  Fq x, y;
+  memcpy(x.v, p.x, 48);
+  memcpy(y.v, p.y, 48);
+  require(zk::fq_is_canonical(x) && zk::fq_is_canonical(y), "point coordinate >= modulus");
+  if (zk::fq_is_zero(x) && zk::fq_is_zero(y)) return {zk::fq_zero(), zk::fq_zero()};
+  const G1A a{zk::fq_to_mont(x), zk::fq_to_mont(y)};
+  Fq four = zk::fq_zero();
+  four.v[0] = 4;
+  const Fq rhs = zk::fq_add(zk::fq_mul(zk::fq_sqr(a.x), a.x), zk::fq_to_mont(four));
+  require(zk::fq_eq(zk::fq_sqr(a.y), rhs), "point not on the curve");
+  return a;
+}
+
+// G2 (canonical affine over Fq2, all zero = infinity) <-> Montgomery, checked on the twist
+zk::G2A parse_g2(const zk_g2& p) {
+  Fq c[4];
+  memcpy(c[0].v, p.x[0], 48);
+  memcpy(c[1].v, p.x[1], 48);
+  memcpy(c[2].v, p.y[0], 48);
+  memcpy(c[3].v, p.y[1], 48);
+  bool zero = true;
+  for (auto& e : c) {
+    require(zk::fq_is_canonical(e), "G2 coordinate >= modulus");
+    zero = zero && zk::fq_is_zero(e);
+    e = zk::fq_to_mont(e);
+  }
+  if (zero) return {zk::fq2_zero(), zk::fq2_zero(), true};
+  const zk::G2A a{{c[0], c[1]}, {c[2], c[3]}, false};
+  require(zk::g2_on_curve(a), "G2 point not on the twist");
+  return a;
+}
+zk_g2 g2_out(const zk::G2A& a) {
+  zk_g2 r;
+  memset(&r, 0, sizeof r);
+  if (a.inf) return r;
+  const Fq c[4] = {zk::fq_from_mont(a.x.c0), zk::fq_from_mont(a.x.c1), zk::fq_from_mont(a.y.c0),
+                   zk::fq_from_mont(a.y.c1)};
+  memcpy(r.x[0], c[0].v, 48);
+  memcpy(r.x[1], c[1].v, 48);
+  memcpy(r.y[0], c[2].v, 48);
+  memcpy(r.y[1], c[3].v, 48);
+  return r;
+}
+
+// Fr scalar (host, repr) -> canonical little-endian u32 limbs (into_bigint)
+void fr_canon(zk_repr repr, const zk_fe& s, uint32_t out[8]) {
+  const Fe c = zk::fe_from_mont<Fr381>(in_mont<Fr381>(repr, s));
+  memcpy(out, c.v, 32);
+}
+
+// G1 affine (Montgomery) of a Jacobian point
+G1A g1_affine(const G1J& p) { return zk::g1_to_affine(p); }
+
 // Fr values (host, repr) -> canonical Fr on the device (k_check_canonical + conversion)
 void upload_fr_canonical(zk_ctx* c, zk_repr repr, const zk_fe* host, uint64_t n, Fe* dev) {
   upload<Fr381>(c, repr, host, n, dev);  // -> Montgomery, checked < r
@@ -273,6 +331,17 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
     jac.ensure(N * sizeof(G1J));
     launch(c, ZK_K_MSM, 176.0 * N, 0, zk::k_fixed_base, grid_for(c, N, zk::k_fixed_base), table,
            (const Fe*)sc.p, N, dptr<G1J>(jac));
+    // G2 half of run_trusted_setup (:43-46): tau_i * G2, on the host (nvars
+    // scalar multiplications) while the basis kernels run
+    {
+      const zk::G2J g2 = zk::g2_from_affine(zk::g2_generator());
+      k->g2_taus.resize(nvars);
+      for (uint32_t i = 0; i < nvars; ++i) {
+        uint32_t t[8];
+        fr_canon(repr, taus[i], t);
+        k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, t));
+      }
+    }
     for (uint32_t v = nvars + 1; v-- > 0;) {
       const uint64_t n = (uint64_t)1 << v;
       if (v < nvars)
@@ -350,28 +419,91 @@ int zk_msm_g1(zk_ctx* c, zk_repr repr, const zk_g1* bases, const zk_fe* scalars,
     require(c && out && (n == 0 || (bases && scalars)), "null argument");
     bind(c);
     std::vector<G1A> b(n);
-    for (size_t i = 0; i < n; ++i) {
-      Fq x, y;
-      memcpy(x.v, bases[i].x, 48);
-      memcpy(y.v, bases[i].y, 48);
-      require(zk::fq_is_canonical(x) && zk::fq_is_canonical(y), "point coordinate >= modulus");
-      if (zk::fq_is_zero(x) && zk::fq_is_zero(y)) {
-        b[i] = {zk::fq_zero(), zk::fq_zero()};
-      } else {
-        b[i] = {zk::fq_to_mont(x), zk::fq_to_mont(y)};
-        const Fq lhs = zk::fq_sqr(b[i].y);
-        Fq four = zk::fq_zero();
-        four.v[0] = 4;
-        const Fq rhs = zk::fq_add(zk::fq_mul(zk::fq_sqr(b[i].x), b[i].x), zk::fq_to_mont(four));
-        require(zk::fq_eq(lhs, rhs), "point not on the curve");
-      }
-    }
+    for (size_t i = 0; i < n; ++i) b[i] = parse_g1(bases[i]);
     DevBuf& db = c->msm[9];
     db.ensure(std::max<size_t>(1, n) * sizeof(G1A));
     if (n) HIPCK(hipMemcpyAsync(db.p, b.data(), n * sizeof(G1A), hipMemcpyHostToDevice, c->stream));
     c->input.ensure(std::max<size_t>(1, n) * 32);
     upload_fr_canonical(c, repr, scalars, n, c->input.fe());
     *out = g1_out(msm_g1_device(c, dptr<G1A>(db), c->input.fe(), n));
+  });
+}
+
+// ---- KZG verifier half: G2 taus and the pairing (host; pairing.hpp) ----
+int zk_kzg_g2_taus(const zk_kzg* k, zk_g2* out) {
+  return guarded([&] {
+    require(k && out, "null argument");
+    for (uint32_t i = 0; i < k->nv; ++i) out[i] = g2_out(k->g2_taus[i]);
+  });
+}
+
+int zk_g2_mul_generator(zk_repr repr, const zk_fe* scalars, size_t n, zk_g2* out) {
+  return guarded([&] {
+    require(n == 0 || (scalars && out), "null argument");
+    const zk::G2J g2 = zk::g2_from_affine(zk::g2_generator());
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t s[8];
+      fr_canon(repr, scalars[i], s);
+      out[i] = g2_out(zk::g2_to_affine(zk::g2_mul(g2, s)));
+    }
+  });
+}
+
+int zk_bls12_381_pairing(const zk_g1* p, const zk_g2* q, uint64_t out[72]) {
+  return guarded([&] {
+    require(p && q && out, "null argument");
+    const zk::Fq12 e = zk::multi_pairing({parse_g1(*p)}, {parse_g2(*q)});
+    const zk::Fq2* c[6] = {&e.c0.c0, &e.c0.c1, &e.c0.c2, &e.c1.c0, &e.c1.c1, &e.c1.c2};
+    for (int i = 0; i < 6; ++i) {
+      const Fq a = zk::fq_from_mont(c[i]->c0), b = zk::fq_from_mont(c[i]->c1);
+      memcpy(out + 12 * i, a.v, 48);
+      memcpy(out + 12 * i + 6, b.v, 48);
+    }
+  });
+}
+
+int zk_bls12_381_pairing_check(const zk_g1* p, const zk_g2* q, size_t n, int* out_ok) {
+  return guarded([&] {
+    require(out_ok && (n == 0 || (p && q)), "null argument");
+    std::vector<G1A> P(n);
+    std::vector<zk::G2A> Q(n);
+    for (size_t i = 0; i < n; ++i) {
+      P[i] = parse_g1(p[i]);
+      Q[i] = parse_g2(q[i]);
+    }
+    *out_ok = zk::fq12_is_one(zk::multi_pairing(P, Q)) ? 1 : 0;
+  });
+}
+
+// KZG::verify (kzg.rs:97-129): e(C - v G1, G2) == sum_i e(q_i, g2_taus[i] - a_i G2)
+// (GT written additively in ark), checked as one product of Miller loops
+// e(C - v G1, G2) * prod_i e(-q_i, g2_taus[i] - a_i G2) with one final
+// exponentiation — the same boolean.
+int zk_kzg_verify(zk_repr repr, const zk_g1* commitment, const zk_fe* opened_value, const zk_g1* proof,
+                  uint32_t nproof, const zk_fe* point, uint32_t npoint, const zk_g2* g2_taus, int* out_verified) {
+  return guarded([&] {
+    require(commitment && opened_value && out_verified && ((proof && point && g2_taus) || npoint == 0),
+            "null argument");
+    // :104-106
+    require(nproof == npoint, "num of quotients in proof not equal to num of opening values");
+    using namespace zk;
+    const G1J g1 = g1_from_affine(g1_generator());
+    const G2J g2 = g2_from_affine(g2_generator());
+    uint32_t v[8];
+    fr_canon(repr, *opened_value, v);
+    const G1J lhs = g1_add(g1_from_affine(parse_g1(*commitment)), g1_neg(g1_mul(g1, v)));
+    std::vector<G1A> P{g1_affine(lhs)};
+    std::vector<G2A> Q{g2_generator()};
+    for (uint32_t i = 0; i < npoint; ++i) {
+      uint32_t a[8];
+      fr_canon(repr, point[i], a);
+      const G2J factor = g2_add(g2_from_affine(parse_g2(g2_taus[i])), g2_neg(g2_mul(g2, a)));
+      G1A qi = parse_g1(proof[i]);
+      if (!g1a_is_inf(qi)) qi.y = fq_neg(qi.y);
+      P.push_back(qi);
+      Q.push_back(g2_to_affine(factor));
+    }
+    *out_verified = fq12_is_one(multi_pairing(P, Q)) ? 1 : 0;
   });
 }
 

@@ -74,6 +74,11 @@ SIGNATURES = {
     "zk_dev_kzg_commit": (I, [P, P, P, P]),
     "zk_kzg_get_proof": (I, [P, P, I, P, P, P, P]),
     "zk_msm_g1": (I, [P, I, P, P, SZ, P]),
+    "zk_kzg_g2_taus": (I, [P, P]),
+    "zk_kzg_verify": (I, [I, P, P, P, U32, P, U32, P, C.POINTER(C.c_int)]),
+    "zk_g2_mul_generator": (I, [I, P, SZ, P]),
+    "zk_bls12_381_pairing": (I, [P, P, P]),
+    "zk_bls12_381_pairing_check": (I, [P, P, SZ, C.POINTER(C.c_int)]),
     "zk_gkr_proof_to_blob": (I, [I, I, P, P, U32, P, P, SZ, C.POINTER(SZ)]),
     "zk_sumcheck_proof_to_blob": (I, [I, I, P, U32, U32, P, P, SZ, C.POINTER(SZ)]),
     "zk_proof_blob_info": (I, [P, SZ, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(U32)]),
