@@ -338,7 +338,7 @@ def main() -> None:
             # during the LAST timed step only: their marker packets cost the GPU
             # ~5 us per round, so timing every step would inflate ms_per_step
             st0 = ctx.stats()
-            ctx.set_timing_kinds([] if args.no_events else ["gkr_round"])
+            ctx.set_timing_kinds([] if args.no_events else ["gkr_round", "gkr_round_lanes"])
         step()
     torch.cuda.synchronize()
     barrier()
@@ -355,9 +355,14 @@ def main() -> None:
     value = ops / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     k = st["kernels"]
-    # the dominant kernel over the event-timed (last) step
-    rnd = {f: k["gkr_round"][f] - st0["kernels"]["gkr_round"][f] for f in ("launches", "alg_bytes")}
-    rnd["ms"] = k["gkr_round"]["ms"]
+    # the dominant kernel (k_gkr_round: the large rounds) and the small rounds'
+    # k_gkr_round_lanes, over the event-timed (last) step
+    def kind(name):
+        d = {f: k[name][f] - st0["kernels"][name][f] for f in ("launches", "alg_bytes")}
+        d["ms"] = k[name]["ms"]
+        return d
+
+    rnd, lanes = kind("gkr_round"), kind("gkr_round_lanes")
     achieved = rnd["alg_bytes"] / (rnd["ms"] / 1e3) / 1e9 if rnd["ms"] else 0.0
     kernel_ms = sum(v["ms"] for v in k.values())  # the timed (last) step
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
@@ -366,8 +371,9 @@ def main() -> None:
     tpath = os.path.join(ROOT, "profiles", "r1_traffic.json")
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
-        traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
-        traffic_src = f"profiles/r1_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
+        if t.get("kernel") == "k_gkr_round" and field == 0:  # per-symbol summary of this workload
+            traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
+            traffic_src = f"profiles/r1_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
     if rank == 0:
         out = {
             "metric": "GKR sum-check field-ops/sec + prover ms, 24-var BN254, 1/2/4/8 GPU",
@@ -393,7 +399,7 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gkr_round (fused fold + round evaluation)",
+                "kernel": "k_gkr_round (fused fold + round evaluation; rounds with > 2^15 pairs)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -404,6 +410,14 @@ def main() -> None:
                 "avg_launch_us": rnd["ms"] * 1e3 / max(1, rnd["launches"]),
                 "alg_bytes_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]),
                 "alg_GB_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]) / 1e9,
+                "small_rounds": {
+                    "kernel": "k_gkr_round_lanes (rounds with <= 2^15 pairs, latency-bound)",
+                    "launches": lanes["launches"],
+                    "avg_launch_us": lanes["ms"] * 1e3 / max(1, lanes["launches"]),
+                    "achieved_GBs": lanes["alg_bytes"] / (lanes["ms"] / 1e3) / 1e9 if lanes["ms"] else None,
+                },
+                "all_rounds_GBs": (rnd["alg_bytes"] + lanes["alg_bytes"]) / ((rnd["ms"] + lanes["ms"]) / 1e3) / 1e9
+                if rnd["ms"] + lanes["ms"] else None,
             },
             "breakdown_per_step": {
                 "wall_ms": ms_per_step,

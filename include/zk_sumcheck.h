@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 3u
+#define ZK_ABI_VERSION 4u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -69,7 +69,7 @@ void zk_ctx_destroy(zk_ctx* ctx);
  * ctx stream) is collected only while enabled. */
 enum {
   ZK_K_GKR_ROUND0 = 0, /* first GKR round: e0,e1,e2 over the input tables */
-  ZK_K_GKR_ROUND = 1,  /* fused fold-by-r + next-round e0,e2 over 4 tables */
+  ZK_K_GKR_ROUND = 1,  /* fused fold-by-r + next-round e0,e2 over 4 tables (k_gkr_round) */
   ZK_K_SC_ROUND = 2,   /* plain sum-check: (fold) + half sums */
   ZK_K_FOLD = 3,       /* MultilinearPoly::partial_evaluate */
   ZK_K_REDUCE = 4,     /* block partials -> limb-split sums */
@@ -77,7 +77,8 @@ enum {
   ZK_K_SYNTH = 6,      /* synthetic table generator */
   ZK_K_LAYER = 7,      /* GKR circuit: layer evaluation, gate weights, layer tables */
   ZK_K_MSM = 8,        /* KZG: bucket sort, bucket/window sums, fixed-base setup, normalisation */
-  ZK_K_KINDS = 9
+  ZK_K_GKR_LANES = 9,  /* the same round for small tables, 8 lanes per pair (k_gkr_round_lanes) */
+  ZK_K_KINDS = 10
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];

@@ -299,8 +299,9 @@ def test_stats_and_timing(ctx):
     ctx.set_timing(False)
     st = ctx.stats()
     k = st["kernels"]
-    assert k["gkr_round0"]["launches"] == 1 and k["gkr_round"]["launches"] == n - 1
-    assert k["gkr_round"]["ms"] > 0 and st["host_syncs"] >= n
+    assert k["gkr_round0"]["launches"] == 1 and k["gkr_round"]["launches"] + k["gkr_round_lanes"]["launches"] == n - 1
+    assert k["gkr_round_lanes"]["launches"] > 0  # rounds with <= 2^15 pairs
+    assert k["gkr_round_lanes"]["ms"] > 0 and st["host_syncs"] >= n
     assert k["gkr_round0"]["alg_bytes"] == 256 * (1 << (n - 1))
 
 

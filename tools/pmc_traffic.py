@@ -39,11 +39,22 @@ def main():
         pairs = 1 << (nvars - 1 - k)
         per_round.append({"round": k, "kernel": name.split("(")[0], "fetch_bytes": 2 * fe * 1024,
                           "write_bytes": wr * 1024, "alg_bytes": 768.0 * pairs})
-    tot_traffic = sum(r["fetch_bytes"] + r["write_bytes"] for r in per_round)
-    tot_alg = sum(r["alg_bytes"] for r in per_round)
-    res = {"kernel": "k_gkr_round (+ k_gkr_round_lanes)", "nvars": nvars, "launches": rounds,
-           "traffic_bytes_per_launch": tot_traffic / rounds, "alg_bytes_per_launch": tot_alg / rounds,
+    # the dominant kernel is the symbol k_gkr_round (large rounds); the small
+    # rounds' k_gkr_round_lanes is summarised beside it
+    def summary(sym):
+        rs = [r for r in per_round if r["kernel"].endswith(sym)]
+        t = sum(r["fetch_bytes"] + r["write_bytes"] for r in rs)
+        a = sum(r["alg_bytes"] for r in rs)
+        return rs, t, a
+
+    big, tot_traffic, tot_alg = summary("k_gkr_round<zk::Bn254Fr>")
+    lanes, lt, la = summary("k_gkr_round_lanes<zk::Bn254Fr>")
+    res = {"kernel": "k_gkr_round", "nvars": nvars, "launches": len(big),
+           "traffic_bytes_per_launch": tot_traffic / len(big), "alg_bytes_per_launch": tot_alg / len(big),
            "traffic_over_alg": tot_traffic / tot_alg,
+           "lanes": {"kernel": "k_gkr_round_lanes", "launches": len(lanes),
+                     "traffic_bytes_per_launch": lt / max(1, len(lanes)), "alg_bytes_per_launch": la / max(1, len(lanes)),
+                     "traffic_over_alg": lt / la if la else None},
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 half-count correction)",
            "per_round": per_round}

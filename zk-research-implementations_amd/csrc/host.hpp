@@ -498,7 +498,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     if (h <= c->lanes_max_pairs) {  // latency-bound size: 8 lanes per pair
       const uint32_t g8 = grid_for(c, 8 * h, zk::k_gkr_round_lanes<F>);
-      launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round_lanes<F>, g8, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
+      launch(c, ZK_K_GKR_LANES, 768.0 * h, 12.0 * h, zk::k_gkr_round_lanes<F>, g8, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
     } else {
       const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round<F>);
       launch(c, ZK_K_GKR_ROUND, 768.0 * h, 12.0 * h, zk::k_gkr_round<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1], nx[2], nx[3], h, rin, sk);
