@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 4u
+#define ZK_ABI_VERSION 6u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -78,7 +78,9 @@ enum {
   ZK_K_LAYER = 7,      /* GKR circuit: layer evaluation, gate weights, layer tables */
   ZK_K_MSM = 8,        /* KZG: bucket sort, bucket/window sums, fixed-base setup, normalisation */
   ZK_K_GKR_LANES = 9,  /* the same round for small tables, 8 lanes per pair (k_gkr_round_lanes) */
-  ZK_K_KINDS = 10
+  ZK_K_GKR_TAIL = 10,  /* the small rounds of a proof in one persistent kernel (k_gkr_tail, ZK_DROUND=0) */
+  ZK_K_GKR_DROUND = 11, /* two rounds per kernel: pending folds + round sums + next round's quadratics (k_gkr_dround) */
+  ZK_K_KINDS = 12
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().zk_abi_version() == 4
+    assert _lib.lib().zk_abi_version() == 6
 
 
 def test_nm_exports_match_header():
@@ -163,3 +163,15 @@ def test_single_hip_runtime_in_process():
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.startswith("1 "), out.stdout
     assert "free()" not in out.stderr and "double free" not in out.stderr, out.stderr[-2000:]
+
+
+def test_kernel_kinds_match_header():
+    """The ctypes zk_stats mirror is sized by KERNEL_KINDS: it must list exactly
+    the header's ZK_K_* kinds, in order (a short mirror lets zk_ctx_get_stats
+    write past the Python struct)."""
+    text = open(HEADER).read()
+    kinds = dict((m.group(1).lower(), int(m.group(2))) for m in re.finditer(r"ZK_K_([A-Z0-9_]+) = (\d+)", text))
+    total = kinds.pop("kinds")
+    assert total == len(_lib.KERNEL_KINDS)
+    alias = {"gkr_lanes": "gkr_round_lanes"}  # header name -> mirror name
+    assert [alias.get(k, k) for k in sorted(kinds, key=kinds.get)] == _lib.KERNEL_KINDS

@@ -3,6 +3,12 @@
 
 * The proof is identical with and without pre-enqueue (ZK_PRELAUNCH=0 launches
   each round after its challenge), and equal to the oracle's.
+* From round 2 on two rounds run per kernel (k_gkr_dround, default); the
+  proof is identical with one round per kernel (ZK_DROUND=0), for odd and
+  even round counts, pre-enqueued or not.
+* With ZK_DROUND=0 the small rounds run in one persistent kernel (k_gkr_tail);
+  the proof is identical with one launch per round (ZK_TAIL=0) and when the
+  tail starts at round 1 over large tables (ZK_LANES_MAX_PAIRS).
 * When the host fails mid-proof (here: the host all-reduce callback raises in
   round 3), the call returns ZK_ECOMM promptly — the guard releases every
   kernel still waiting instead of letting each run into its 1 s limit — and
@@ -54,6 +60,58 @@ def test_prelaunch_and_per_round_launch_agree(monkeypatch, field):
             assert _prove(ctx, field, n) == want, f"ZK_PRELAUNCH={mode}"
         finally:
             ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("tail,lanes_max", [("1", None), ("0", None), ("1", str(1 << 20)), ("1", "4")])
+def test_tail_kernel_modes_agree(monkeypatch, field, tail, lanes_max):
+    n = 17 if lanes_max is None else 21
+    want = _oracle(field, n) if n == 17 else None
+    monkeypatch.setenv("ZK_DROUND", "0")
+    monkeypatch.setenv("ZK_TAIL", tail)
+    if lanes_max is not None:
+        monkeypatch.setenv("ZK_LANES_MAX_PAIRS", lanes_max)
+    ctx = zk_amd.Context(0)
+    try:
+        got = _prove(ctx, field, n)
+        if want is None:  # compare with the per-round launches of the same context settings
+            monkeypatch.setenv("ZK_TAIL", "0")
+            ref = zk_amd.Context(0)
+            try:
+                want = _prove(ref, field, n)
+            finally:
+                ref.close()
+        assert got == want
+        assert _prove(ctx, field, n) == want  # reused tail buffer and relay slots
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 9, 12, 15])
+def test_double_rounds_match_oracle(monkeypatch, field, n):
+    want = _oracle(field, n)
+    for pre in ("1", "0"):
+        monkeypatch.setenv("ZK_PRELAUNCH", pre)
+        ctx = zk_amd.Context(0)
+        try:
+            assert _prove(ctx, field, n) == want, f"ZK_PRELAUNCH={pre}"
+        finally:
+            ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 2])
+def test_double_and_single_rounds_agree_20var(monkeypatch, field):
+    n = 20
+    got = {}
+    for dr in ("1", "0"):
+        monkeypatch.setenv("ZK_DROUND", dr)
+        ctx = zk_amd.Context(0)
+        try:
+            got[dr] = _prove(ctx, field, n)
+        finally:
+            ctx.close()
+    assert got["1"] == got["0"]
 
 
 def test_host_failure_mid_proof_releases_waiting_rounds(monkeypatch):

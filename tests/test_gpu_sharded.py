@@ -59,7 +59,15 @@ def _oracle(field: int, n: int) -> dict:
             "blob_keccak": po.keccak256(po.proof_blob(po.BLOB_GKR, field, 0, [list(p) for p in polys])).hex()}
 
 
-@pytest.mark.parametrize("world,nloc,field", [(2, 12, 0), (4, 9, 2), (2, 0, 1)])
+def _steps(nloc: int) -> int:
+    """Kernel steps of a phase of nloc rounds, one all-reduce each: round 0,
+    round 1, one more single round if nloc - 2 is odd, then two rounds per step."""
+    if nloc <= 2:
+        return nloc
+    return 2 + (nloc - 2) % 2 + (nloc - 2) // 2
+
+
+@pytest.mark.parametrize("world,nloc,field", [(2, 12, 0), (4, 9, 2), (2, 0, 1), (2, 5, 0)])
 def test_host_comm_ranks_match_single_process(tmp_path, world, nloc, field):
     res = _run(world, "host", field, nloc, str(tmp_path))
     want = _oracle(field, nloc + world.bit_length() - 1)
@@ -67,7 +75,7 @@ def test_host_comm_ranks_match_single_process(tmp_path, world, nloc, field):
         assert {"polys": r["polys"], "chal": r["chal"]} == {"polys": want["polys"], "chal": want["chal"]}, f"rank {rank}"
         # f4: the whole proof as one digest, identical on every rank and to the CPU oracle's
         assert r["blob_keccak"] == want["blob_keccak"], f"rank {rank}"
-        assert r["collectives"] == nloc + 1  # one all-reduce per local round + the tail gather
+        assert r["collectives"] == _steps(nloc) + 1  # one all-reduce per step + the tail gather
 
 
 def test_world1_without_comm(tmp_path):
@@ -81,4 +89,4 @@ def test_rccl_data_path_forced_at_world1(tmp_path):
     res = _run(1, "rccl", 0, 14, str(tmp_path), {"ZK_FORCE_COLLECTIVES": "1"})
     want = _oracle(0, 14)
     assert {"polys": res[0]["polys"], "chal": res[0]["chal"], "blob_keccak": res[0]["blob_keccak"]} == want
-    assert res[0]["collectives"] == 14  # every round went through ncclAllReduce
+    assert res[0]["collectives"] == _steps(14)  # every step went through ncclAllReduce

@@ -284,6 +284,60 @@ ZK_HD Fe wide_redc(const Wide& V) {
   return fe_add<F>(lo, fe_mul<F>(hi, r2));  // hi * R mod p
 }
 
+// Fold by two challenges at once (two successive partial_evaluate(0, .) calls,
+// multilinear_polynomial_evaluation.rs:52-63): for the four table entries
+// x_ab (a = first folded variable, b = second)
+//   Z = x00 + ra (x10 - x00) + rb (x01 - x00) + ra rb (x11 - x10 - x01 + x00)
+// The three products are summed unreduced and reduced by ONE REDC: 3 x 64 +
+// 64 mads instead of 3 chained Montgomery multiplies (3 x 128). rab = ra*rb.
+// The sum W < 3 p^2 < 2^512 (p < 2^255), so REDC(W) < W / 2^256 + p < 3p and
+// fits 9 words; two conditional subtractions bring it into [0, p).
+template <class F>
+ZK_HD Fe redc3p(const Wide& W) {
+  uint32_t t[17];
+#pragma unroll
+  for (int k = 0; k < 17; ++k) t[k] = W.w[k];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t m = t[i] * F::PINV;
+    uint64_t Q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Q[j] = mad64(m, F::P[j], t[i + j]);
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) t[i + j] = addc32((uint32_t)Q[j], (uint32_t)(Q[j - 1] >> 32), c, &c);
+    t[i + 8] = addc32(t[i + 8], (uint32_t)(Q[7] >> 32), c, &c);
+#pragma unroll
+    for (int q = i + 9; q < 17; ++q) t[q] = addc32(t[q], 0u, c, &c);
+  }
+  // V = t[8..16] < 3p: subtract p while V >= p (at most twice)
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    uint32_t d[9], b = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = subb32(t[8 + k], F::P[k], b, &b);
+    d[8] = subb32(t[16], 0u, b, &b);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) t[8 + k] = b ? t[8 + k] : d[k];
+  }
+  Fe r;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r.v[k] = t[8 + k];
+  return r;
+}
+template <class F>
+ZK_HD Fe fold2(const Fe& x00, const Fe& x01, const Fe& x10, const Fe& x11, const Fe& ra, const Fe& rb,
+               const Fe& rab) {
+  const Fe d1 = fe_sub<F>(x10, x00);
+  const Fe d2 = fe_sub<F>(x01, x00);
+  const Fe d3 = fe_sub<F>(fe_sub<F>(x11, x01), d1);
+  Wide w = wide_zero<F>();
+  wide_mac<F>(w, ra, d1);
+  wide_mac<F>(w, rb, d2);
+  wide_mac<F>(w, rab, d3);
+  return fe_add<F>(x00, redc3p<F>(w));
+}
+
 // Limb sums -> field element. w[i] (i < L <= 17) are sums of 32-bit words at
 // weight 2^(32 i) (each < 2^62), i.e. the integer T = sum_i w[i] 2^(32 i) < 2^624.
 // Split T = C0 + C1 R + C2 R^2 (R = 2^256).

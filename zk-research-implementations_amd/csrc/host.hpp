@@ -181,8 +181,9 @@ struct zk_ctx {
   DevBuf work[2];  // ping-pong fold workspaces: 4 tables each
   DevBuf input;    // host-API staging (4 tables)
   DevBuf partials;
+  DevBuf tailbuf;  // k_gkr_tail: 64 relay slots, then the fresh per-round table regions
   DevBuf small;    // round totals (<= 64 u64) + flag + gather buffers
-  uint64_t* h_red = nullptr;  // pinned, device-mapped: round totals (<= 51 u64) + flag word at [64]
+  uint64_t* h_red = nullptr;  // pinned, device-mapped page (kHostPage): round totals, flag, challenge slots
   uint32_t tag = 0;           // last round tag handed to a kernel
   uint64_t lanes_max_pairs = 1u << 15;  // rounds with <= this many pairs use 8 lanes per pair
   std::chrono::steady_clock::time_point work_t0;  // when the last round result was seen
@@ -201,6 +202,10 @@ struct zk_ctx {
   zk_allreduce_u64_fn ar = nullptr;
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
+  bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
+  bool tail = true;         // (ZK_DROUND=0 only) pre-enqueued small rounds in one persistent kernel (ZK_TAIL=0: one launch each)
+  uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
+  uint64_t* tail_trace = nullptr;      // ZK_DEBUG_TAIL: pinned per-round stamps of the tail kernel, printed per proof
   uint32_t rtag = 0;        // last tag handed to a pre-enqueued round kernel
   void* user = nullptr;
   ncclComm_t nccl = nullptr;
@@ -212,24 +217,28 @@ struct zk_ctx {
 
 
 namespace zkh {
-// small device area: [0,512) round sums, [512] input check flag, [1024,2304)
-// fan-in counters (9 x 128 B), [2560,3072) limb accumulator (<= 64 u64),
-// [4096, +64 KiB) all-reduce bounce buffer
+// small device area: [0,2048) round sums (<= 256 u64), [2048] input check
+// flag, [2560,3712) fan-in counters (9 x 128 B), [4096,6144) limb accumulator
+// (<= 256 u64), [6144,6656) single-round relay slots (8 x 64 B), [6656,6912)
+// the double-round relay slot, [8192, +64 KiB) all-reduce bounce buffer
 // (<= 256 ranks x 256 B), then the tail's 4 local elements and the gathered
 // 4 x world tables
 constexpr size_t kSmallBytes = 160 * 1024;
 inline uint64_t* d_red(zk_ctx* c) { return reinterpret_cast<uint64_t*>(c->small.p); }
-inline uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 512); }
-inline uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 1024); }
-inline uint64_t* d_accum(zk_ctx* c) { return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(c->small.p) + 2560); }
-inline uint32_t* h_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(c->h_red + 64); }
-inline char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 4096; }
-// pre-enqueued rounds: the pinned slot the host posts r to, the pinned error
-// word, and the device relay slots (h_red page: [1024, 1088) and [2048];
-// small area: [3072, 3584) = 8 x 64 B)
-inline zk::RWait* h_rin(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->h_red) + 1024); }
-inline uint32_t* h_err(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->h_red) + 2048); }
-inline zk::RWait* d_relay(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->small.p) + 3072); }
+inline uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 2048); }
+inline uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 2560); }
+inline uint64_t* d_accum(zk_ctx* c) { return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(c->small.p) + 4096); }
+inline char* d_gather(zk_ctx* c) { return reinterpret_cast<char*>(c->small.p) + 8192; }
+// pinned, device-mapped host page (8 KiB): [0,2048) round totals, [2048] the
+// result flag, [4096,4160) the single-round challenge slot, [4160] the error
+// word, [6144,6400) the double-round challenge words
+constexpr size_t kHostPage = 8192;
+inline uint32_t* h_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->h_red) + 2048); }
+inline zk::RWait* h_rin(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->h_red) + 4096); }
+inline uint32_t* h_err(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->h_red) + 4160); }
+inline zk::RPost* h_rpost(zk_ctx* c) { return reinterpret_cast<zk::RPost*>(reinterpret_cast<char*>(c->h_red) + 6144); }
+inline zk::RWait* d_relay(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->small.p) + 6144); }
+inline zk::RPost* d_rpost(zk_ctx* c) { return reinterpret_cast<zk::RPost*>(reinterpret_cast<char*>(c->small.p) + 6656); }
 
 inline void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
 
@@ -378,7 +387,7 @@ inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks
   if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
     NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
     c->stats.collectives += 1;
-    zk::k_publish<<<1, 64, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
+    zk::k_publish<<<1, 256, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
     HIPCK(hipGetLastError());
   }
 }
@@ -390,7 +399,7 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
   wait_flag(c, sk.tag);
   if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) != 0)
     fail(ZK_EDEVICE, "a pre-enqueued round kernel waited more than 1 s for its challenge");
-  uint64_t w[K * 17];
+  uint64_t w[K * 17 > 17 ? K * 17 : 17];
   for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
   if (multi && c->comm == COMM_HOST) {
     if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
@@ -446,9 +455,20 @@ struct PostR {
     for (int i = 0; i < 8; ++i) __atomic_store_n(&s->r.v[i], r.v[i], __ATOMIC_RELAXED);
     __atomic_store_n(&s->tag, tag, __ATOMIC_RELEASE);
   }
+  // the double-round slot: 24 self-tagged words (tag << 32 | limb), any order
+  void post2(const Fe& ra, const Fe& rb, const Fe& rab, uint32_t tag) {
+    zk::RPost* s = h_rpost(c);
+    const uint64_t t = (uint64_t)tag << 32;
+    for (int i = 0; i < 8; ++i) {
+      __atomic_store_n(&s->w[i], t | ra.v[i], __ATOMIC_RELAXED);
+      __atomic_store_n(&s->w[8 + i], t | rb.v[i], __ATOMIC_RELAXED);
+      __atomic_store_n(&s->w[16 + i], t | rab.v[i], __ATOMIC_RELAXED);
+    }
+  }
   ~PostR() {
     if (done || last == 0) return;
     post(zk::fe_zero<zk::Bn254Fr>(), last);
+    post2(zk::fe_zero<zk::Bn254Fr>(), zk::fe_zero<zk::Bn254Fr>(), zk::fe_zero<zk::Bn254Fr>(), last);
     (void)hipStreamSynchronize(c->stream);
   }
 };
@@ -457,44 +477,159 @@ struct PostR {
 inline bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1; }
 
 // Run `nv` rounds over 4 device tables of 2^nv elements starting at global
-// round k0. The first round of a phase computes e0,e1,e2 directly; later
-// rounds fold by the previous challenge in the same kernel. On return `cur`
-// points at the (unfolded) size-2 tables of the last round.
-// Pre-enqueued (default): every round kernel (and, across ranks over RCCL,
-// its all-reduce + publish) is enqueued before round 0's sums are read;
-// round i's kernel waits in-kernel for r_{i-1}, which the host posts as soon
-// as it has run the transcript. Otherwise each round is launched after the
-// previous challenge is known.
+// round k0, as a sequence of steps:
+//   round 0        k_gkr_round0: e0, e1, e2 on the input tables;
+//   single round i k_gkr_round / k_gkr_round_lanes: fold by r_{i-1}, e0, e2;
+//   double (i,i+1) k_gkr_dround: apply the pending challenges, rounds i and
+//                  i+1 from one pass (default from round 2 on; an odd count
+//                  of remaining rounds puts one single round first);
+//   tail           (ZK_DROUND=0) k_gkr_tail: the small rounds in one kernel.
+// e1 of every round after the first is derived on the host as
+// s_{k-1}(r_{k-1}) - e0, exact because A*S + M*P has degree 2 per variable.
+// Pre-enqueued (default): every step (and, across ranks over RCCL, its
+// all-reduce + publish) is enqueued before round 0's sums are read; each
+// waits in-kernel for the challenges the host posts. On return `cur` holds
+// tables of 2^pend elements with the last `pend` challenges not yet applied.
+// Small rounds in one persistent kernel (k_gkr_tail, ZK_DROUND=0 only)?
+// Pre-enqueued only, and not when each round's sums take an RCCL all-reduce
+// on the stream (the kernel would hold the stream).
+inline bool use_tail(zk_ctx* c, bool across_ranks) {
+  return c->tail && !(across_ranks && multi_rank(c) && c->comm == COMM_RCCL);
+}
+constexpr size_t kTailRelayBytes = 64 * sizeof(zk::RWait);
+inline size_t tail_bytes(uint64_t h0) { return kTailRelayBytes + 16 * h0 * sizeof(Fe); }
+
+struct GStep {
+  int kind;    // 0 round 0, 1 single, 2 double, 3 tail
+  uint32_t i;  // first round (local)
+  int np;      // double: pending challenges at entry (1 or 2)
+};
+enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3 };
+
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
-               GkrOut& out, Fe& claim, Fe& r) {
+               GkrOut& out, Fe& claim, Fe& r, uint32_t& pend) {
   const uint64_t L = (uint64_t)1 << nv;
   const bool pre = prelaunch(c, nv);
-  std::vector<zk::RoundSink> sinks(nv);
-  std::vector<uint32_t> rtags(nv, 0);
-  auto enqueue = [&](uint32_t i) {
-    const uint64_t size = L >> i;  // table length in this round
+  std::vector<GStep> steps;
+  if (nv >= 1) steps.push_back({GS_ROUND0, 0, 0});
+  if (c->dround) {
+    uint32_t i = 1;
+    if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
+    if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
+    for (int np = 1; i + 1 < nv; i += 2, np = 2) steps.push_back({GS_DOUBLE, i, np});
+  } else {
+    // first round >= 1 with <= tail_max_pairs pairs, if at least two rounds remain
+    uint32_t tail0 = nv;
+    if (pre && use_tail(c, across_ranks)) {
+      uint32_t i = 1;
+      while (i < nv && (L >> i) / 2 > c->tail_max_pairs) ++i;
+      if (i + 2 <= nv && nv - i <= 64) {
+        tail0 = i;
+        const size_t had = c->tailbuf.bytes;
+        c->tailbuf.ensure(tail_bytes((L >> i) / 2));  // before anything of this phase is enqueued
+        if (c->tailbuf.bytes != had) HIPCK(hipMemset(c->tailbuf.p, 0, kTailRelayBytes));  // relay tags at rest
+      }
+    }
+    for (uint32_t i = 1; i < nv; ++i) {
+      if (i == tail0) {
+        steps.push_back({GS_TAIL, i, 0});
+        break;
+      }
+      steps.push_back({GS_SINGLE, i, 0});
+    }
+  }
+  const size_t ns = steps.size();
+  std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
+  std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
+  int inbuf = -1;                        // work buffer holding cur (-1: the input tables)
+  Fe ra = zk::fe_zero<F>(), rb = zk::fe_zero<F>();  // last two challenges (non-pre-enqueued launches)
+  auto out_tables = [&](uint64_t size, Fe* nx[4]) {
+    const int ob = inbuf == 0 ? 1 : 0;
+    Fe* w = c->work[ob].fe();
+    for (int t = 0; t < 4; ++t) nx[t] = w + (uint64_t)t * size;
+    inbuf = ob;
+  };
+  auto enqueue = [&](size_t si) {
+    const GStep& st = steps[si];
+    const uint32_t i = st.i;
+    const uint64_t size = L >> i;  // table length in round i
     const uint64_t h = size / 2;   // pairs
     sinks[i] = make_sink(c, across_ranks);
     const zk::RoundSink& sk = sinks[i];
-    if (i == 0) {
+    if (st.kind == GS_ROUND0) {
       const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round0<F>);
       launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, zk::k_gkr_round0<F>, grid, cur[0], cur[1], cur[2], cur[3], h, sk);
       enqueue_reduce(c, sk, across_ranks, 3 * 17);
       return;
     }
-    // fold previous (size 2*size) -> work[(i+1)&1] (size `size`) and evaluate;
-    // work[0] holds the size-L/2 level, work[1] the size-L/4 level, ...
-    Fe* w = c->work[(i + 1) & 1].fe();
-    Fe* nx[4] = {w, w + size, w + 2 * size, w + 3 * size};
+    if (st.kind == GS_TAIL) {
+      // rounds i .. nv-1: consecutive sink and challenge tags, fresh table
+      // regions in tailbuf (round m: 4 tables of 2 (h >> m) elements)
+      const uint32_t nr = nv - i;
+      for (uint32_t m = 1; m < nr; ++m) sinks[i + m] = make_sink(c, across_ranks);
+      zk::TailArgs a{};
+      for (int t = 0; t < 4; ++t) a.in[t] = cur[t];
+      a.relay = reinterpret_cast<zk::RWait*>(c->tailbuf.p);
+      a.out = reinterpret_cast<Fe*>(reinterpret_cast<char*>(c->tailbuf.p) + kTailRelayBytes);
+      a.h0 = h;
+      a.nrounds = nr;
+      a.host = h_rin(c);
+      a.err = h_err(c);
+      rtags[si] = c->rtag + 1;
+      c->rtag += nr;
+      a.rtag0 = rtags[si];
+      if (c->tail_trace) a.trace = reinterpret_cast<uint64_t*>(c->tail_trace);
+      const uint64_t want = (8 * h + zk::kBlock - 1) / zk::kBlock;
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)c->num_cus);  // one block per CU: co-resident
+      const double pairs = (double)(2 * h - (h >> (nr - 1)));
+      launch(c, ZK_K_GKR_TAIL, 768.0 * pairs, 12.0 * pairs, zk::k_gkr_tail<F>, grid, a, sk);
+      const uint64_t hl = h >> (nr - 1);  // pairs of the last round
+      Fe* last = a.out + zk::tail_region(h, nr - 1);
+      for (int t = 0; t < 4; ++t) cur[t] = last + (uint64_t)t * 2 * hl;
+      return;
+    }
+    if (st.kind == GS_DOUBLE) {
+      // input: level i - np (size << np), output Z: level i (size = 4Q)
+      const uint64_t Q = size / 4;
+      Fe* nx[4];
+      out_tables(size, nx);
+      zk::DIn din{};
+      if (pre) {
+        din.host = h_rpost(c);
+        din.relay = d_rpost(c);
+        din.err = h_err(c);
+        din.tag = rtags[si] = ++c->rtag;
+      } else if (st.np == 2) {
+        din.ra = ra;
+        din.rb = rb;
+        din.rab = zk::fe_mul<F>(ra, rb);
+      } else {
+        din.rb = rb;
+      }
+      const uint32_t grid = grid_for(c, 8 * Q, zk::k_gkr_dround<F, 2>);
+      const double bytes = (st.np == 2 ? 2560.0 : 1536.0) * Q, muls = (st.np == 2 ? 41.0 : 25.0) * Q;
+      if (st.np == 2)
+        launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dround<F, 2>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
+               nx[1], nx[2], nx[3], Q, din, sk);
+      else
+        launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dround<F, 1>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
+               nx[1], nx[2], nx[3], Q, din, sk);
+      for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+      enqueue_reduce(c, sk, across_ranks, zk::kDLimbs);
+      return;
+    }
+    // single round i: fold the previous level (size 2*size) by r_{i-1} and evaluate
+    Fe* nx[4];
+    out_tables(size, nx);
     zk::RoundIn rin{};
     if (pre) {
       rin.host = h_rin(c);
       rin.relay = d_relay(c);
       rin.err = h_err(c);
-      rin.tag = rtags[i] = ++c->rtag;
+      rin.tag = rtags[si] = ++c->rtag;
     } else {
-      rin.r = r;
+      rin.r = rb;
     }
     if (h <= c->lanes_max_pairs) {  // latency-bound size: 8 lanes per pair
       const uint32_t g8 = grid_for(c, 8 * h, zk::k_gkr_round_lanes<F>);
@@ -506,40 +641,89 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     for (int t = 0; t < 4; ++t) cur[t] = nx[t];
     enqueue_reduce(c, sk, across_ranks, 2 * 17);
   };
+  // the highest challenge tag step si (and every step before it) waits for
+  auto last_tag = [&](size_t si) {
+    return steps[si].kind == GS_TAIL ? rtags[si] + (nv - steps[si].i) - 1 : rtags[si];
+  };
   PostR post{c};
   if (pre) {
     const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 0; i < nv; ++i) {
-      enqueue(i);
-      post.last = rtags[i];  // from here on the guard releases what is enqueued
+    for (size_t si = 0; si < ns; ++si) {
+      enqueue(si);
+      post.last = last_tag(si);  // from here on the guard releases what is enqueued
     }
     if (getenv("ZK_DEBUG_ENQUEUE"))
-      fprintf(stderr, "zk: enqueued %u rounds in %.1f us\n", nv,
+      fprintf(stderr, "zk: enqueued %zu steps (%u rounds) in %.1f us\n", ns, nv,
               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
   }
-  for (uint32_t i = 0; i < nv; ++i) {
-    const uint32_t k = k0 + i;
-    if (!pre) enqueue(i);
-    Fe e0, e1, e2;
-    if (i == 0) {
-      Fe s[3];
-      collect_sums<F, 3>(c, sinks[i], across_ranks, 17, s);
-      e0 = s[0];
-      e1 = s[1];
-      e2 = s[2];
+  // hand the newest challenge(s) to step si + 1
+  auto hand_on = [&](size_t si) {
+    if (!pre || si + 1 >= ns) return;
+    const GStep& nx = steps[si + 1];
+    if (nx.kind == GS_DOUBLE) {
+      if (nx.np == 2)
+        post.post2(ra, rb, zk::fe_mul<F>(ra, rb), rtags[si + 1]);
+      else
+        post.post2(zk::fe_zero<F>(), rb, zk::fe_zero<F>(), rtags[si + 1]);
     } else {
-      Fe s[2];
-      collect_sums<F, 2>(c, sinks[i], across_ranks, 17, s);
-      e0 = s[0];
-      e2 = s[1];
-      // s_{k-1}(X) = sum_j f(X, j) is exact (degree 2 in X), so
-      // e0 + e1 = s_{k-1}(r_{k-1}) on the folded tables.
-      e1 = zk::fe_sub<F>(claim, e0);
+      post.post(rb, rtags[si + 1]);
     }
-    claim = finish_round<F>(tr, e0, e1, e2, k, out, r);
-    if (pre && i + 1 < nv) post.post(r, rtags[i + 1]);
+  };
+  auto one_round = [&](uint32_t i, const Fe& e0, const Fe& e1, const Fe& e2) {
+    claim = finish_round<F>(tr, e0, e1, e2, k0 + i, out, r);
+    ra = rb;
+    rb = r;
+  };
+  for (size_t si = 0; si < ns; ++si) {
+    const GStep& st = steps[si];
+    if (!pre) enqueue(si);
+    if (st.kind == GS_ROUND0) {
+      Fe s3[3];
+      collect_sums<F, 3>(c, sinks[0], across_ranks, 17, s3);
+      one_round(0, s3[0], s3[1], s3[2]);
+      pend = 1;
+    } else if (st.kind == GS_SINGLE) {
+      Fe s2[2];
+      collect_sums<F, 2>(c, sinks[st.i], across_ranks, 17, s2);
+      one_round(st.i, s2[0], zk::fe_sub<F>(claim, s2[0]), s2[1]);
+      pend = 1;
+    } else if (st.kind == GS_TAIL) {
+      for (uint32_t i = st.i; i < nv; ++i) {
+        Fe s2[2];
+        collect_sums<F, 2>(c, sinks[i], across_ranks, 17, s2);
+        one_round(i, s2[0], zk::fe_sub<F>(claim, s2[0]), s2[1]);
+        if (pre && i + 1 < nv) post.post(r, rtags[si] + (i + 1 - st.i));
+      }
+      pend = 1;
+    } else {
+      Fe d[zk::kDCats];
+      collect_sums<F, zk::kDCats>(c, sinks[st.i], across_ranks, 17, d);
+      // round i on Z: e0 = alpha + delta, e2
+      const Fe e0 = zk::fe_add<F>(d[0], d[2]);
+      one_round(st.i, e0, zk::fe_sub<F>(claim, e0), d[3]);
+      // round i + 1: sum over (1-r) u + r v = (1-r)^2 Suu + r(1-r)(S(u+v)^2 - Suu - Svv) + r^2 Svv
+      const Fe one = zk::fe_one<F>(), omr = zk::fe_sub<F>(one, r);
+      const Fe c00 = zk::fe_mul<F>(omr, omr), c01 = zk::fe_mul<F>(r, omr), c11 = zk::fe_mul<F>(r, r);
+      auto quad = [&](const Fe& suu, const Fe& suv2, const Fe& svv) {
+        const Fe cross = zk::fe_sub<F>(zk::fe_sub<F>(suv2, suu), svv);
+        return zk::fe_add<F>(zk::fe_add<F>(zk::fe_mul<F>(c00, suu), zk::fe_mul<F>(c01, cross)), zk::fe_mul<F>(c11, svv));
+      };
+      const Fe f0 = quad(d[0], d[1], d[4]), f2 = quad(d[5], d[7], d[6]);
+      one_round(st.i + 1, f0, zk::fe_sub<F>(claim, f0), f2);
+      pend = 2;
+    }
+    hand_on(si);
   }
   post.done = true;
+  if (c->tail_trace && !steps.empty() && steps.back().kind == GS_TAIL) {  // ZK_DEBUG_TAIL
+    HIPCK(hipStreamSynchronize(c->stream));
+    const uint64_t* T = c->tail_trace;
+    const uint32_t nr = nv - steps.back().i;
+    for (uint32_t m = 0; m < nr; ++m)
+      fprintf(stderr, "zk tail round %2u: wait r %6.2f us, fold+eval %6.2f, fan-in %6.2f, publish %6.2f, hand-off to next r %6.2f\n",
+              m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
+              (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, m + 1 < nr ? (T[m * 8 + 9] - T[m * 8 + 4]) * 0.01 : 0.0);
+  }
 }
 
 template <class F>
@@ -560,7 +744,8 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   c->work[1].ensure(4 * std::max<uint64_t>(wmax / 2, 1) * 32);
   const Fe* cur[4] = {dT[0], dT[1], dT[2], dT[3]};
   Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
-  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r);
+  uint32_t pend = 0;
+  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend);
   if (lg == 0) {
     sync(c);  // settles event timings; the results are already on the host
     return;
@@ -571,6 +756,12 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   // each rank fills only its own slot of a zeroed limb-split vector.
   Fe* send = reinterpret_cast<Fe*>(d_gather(c) + 65536);  // 4 elements, after the bounce buffer
   if (nloc > 0) {
+    if (pend == 2) {  // the phase ended on a double round: cur has 4 elements per table, r_{nloc-2} pending too
+      Fe* t2 = send + 4;  // 4 x 2 scratch elements (the staging area below is written after a sync)
+      launch(c, ZK_K_FOLD, 8 * 96.0, 8.0, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], t2, t2 + 2, t2 + 4,
+             t2 + 6, (uint64_t)2, out.challenges[nloc - 2]);
+      for (int t = 0; t < 4; ++t) cur[t] = t2 + 2 * t;
+    }
     Fe* s4[4] = {send, send + 1, send + 2, send + 3};
     launch(c, ZK_K_FOLD, 4 * 96.0, 4.0, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], s4[0], s4[1], s4[2],
            s4[3], (uint64_t)1, r);
@@ -591,7 +782,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   Fe* stage = send + 4;
   HIPCK(hipMemcpyAsync(stage, tabs.data(), tabs.size() * 32, hipMemcpyHostToDevice, c->stream));
   const Fe* tcur[4] = {stage, stage + G, stage + 2 * G, stage + 3 * G};
-  gkr_phase<F>(c, tcur, lg, nloc, false, tr, out, claim, r);
+  gkr_phase<F>(c, tcur, lg, nloc, false, tr, out, claim, r, pend);
   sync(c);
 }
 

@@ -99,7 +99,7 @@ __device__ __forceinline__ Fe at2(const Fe& lo, const Fe& hi) {
 #define ZK_STAMP_AFTER(i, w) do { } while (0)
 #endif
 
-constexpr int kSlotU64 = 64;  // per-block partial slot: up to 64 limb sums (512 B)
+constexpr int kSlotU64 = 160;  // per-block partial slot: up to 160 limb sums (1280 B)
 
 struct RoundSink {
   uint64_t* partials;   // [gridDim.x + 8][kSlotU64]: one slot per block, then 8 shard slots
@@ -250,15 +250,16 @@ __device__ __forceinline__ void block_limb_sums(const Fe& x, Sc& sc, int base) {
 // nothing the host reads was written with plain stores.
 template <int C, class Sc>
 __device__ __forceinline__ void publish_limbs(Sc& sc, const RoundSink& sk) {
-  if (threadIdx.x >= 64) return;
-  const uint32_t lane = threadIdx.x;
-  if (lane < (uint32_t)C) {
-    const uint64_t v = sc.tot[lane];
-    if (sk.dev_out) sk.dev_out[lane] = v;
-    if (sk.host_out) __hip_atomic_store(sk.host_out + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint32_t t = threadIdx.x;
+  if (C <= 64 && t >= 64) return;  // wave 0 alone
+  if (t < (uint32_t)C) {
+    const uint64_t v = sc.tot[t];
+    if (sk.dev_out) sk.dev_out[t] = v;
+    if (sk.host_out) __hip_atomic_store(sk.host_out + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0 && sk.host_flag) __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (C > 64) __syncthreads();  // every storing wave has drained before the flag
+  if (t == 0 && sk.host_flag) __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // sum `count` slots (slot index first + i*stride) of C limb sums -> sc.tot (wave 0 lanes)
@@ -267,8 +268,17 @@ __device__ __forceinline__ void sum_slots(uint64_t* slots, uint32_t first, uint3
   constexpr uint32_t P = kBlock / C;  // parts per column
   const uint32_t t = threadIdx.x, c = t % C, p = t / C;
   uint64_t s = 0;
-  if (p < P)
-    for (uint32_t i = p; i < count; i += P) s += ld_u64_sc1(slots + (uint64_t)(first + i * stride) * kSlotU64 + c);
+  if (p < P) {
+    uint32_t i = p;
+    for (; i + 7 * P < count; i += 8 * P) {  // 8 independent loads in flight
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ld_u64_sc1(slots + (uint64_t)(first + (i + u * P) * stride) * kSlotU64 + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; i < count; i += P) s += ld_u64_sc1(slots + (uint64_t)(first + i * stride) * kSlotU64 + c);
+  }
   sc.pp[t] = s;
   __syncthreads();
   if (t < (uint32_t)C) {
@@ -283,7 +293,7 @@ constexpr uint32_t kAtomicFaninMax = 64;  // grids up to this size fan in throug
 // Block limb sums are in sc.tot[0..C) (valid for threads < C); finish over the grid.
 template <int C, class Sc>
 __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk) {
-  static_assert(C <= kSlotU64 && C <= 64, "limb vector too long");
+  static_assert(C <= kSlotU64 && C <= kBlock, "limb vector too long");
   const uint32_t G = gridDim.x, t = threadIdx.x;
   if (G == 1) {
     ZK_STAMP(4);
@@ -348,10 +358,10 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk) {
   ZK_STAMP(6);
 }
 
-// copy n u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
+// copy n <= 256 u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
 static __global__ void k_publish(const uint64_t* __restrict__ src, int n, uint64_t* host_out, uint32_t* host_flag,
                           uint32_t tag) {
-  if (threadIdx.x < n)
+  if ((int)threadIdx.x < n)
     __hip_atomic_store(host_out + threadIdx.x, src[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -507,6 +517,356 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round_lanes(const Fe* __restrict
   __syncthreads();
   ZK_STAMP(3);
   grid_finish<34>(sc, sink);
+}
+
+// ---------------------------------------------------------------------------
+// The tail of a GKR proof in ONE persistent kernel: the last `nrounds` rounds
+// (pairs h0, h0/2, ..., each round the k_gkr_round_lanes step) without a
+// kernel boundary between them. Per round, block 0 waits for the host-posted
+// challenge (tag rtag0 + m) and relays it; the active blocks fold and
+// evaluate; their limb sums meet in the u64 accumulator; the last block
+// publishes them (sink tag tag0 + m) and the host answers with the next
+// challenge. What a boundary cost each small round — dispatch, the end-of-
+// kernel cache write-back, a cold instruction cache for the 256-bit multiply
+// code — is paid once.
+//
+// Inter-block data (the folded tables of round m, read by other blocks in
+// round m + 1) follows the guide's 8-byte agent-atomics form on both sides
+// (MI355X_MICROARCH.md "Valid forms"): every store and every load of those
+// bytes is a relaxed agent-scope 8-B atomic (sc1), every storing wave drains
+// (vmcnt(0)) before its block's counter add, and a consumer only loads after
+// the relayed challenge, which the host posts after the last block's publish.
+// Each round writes a fresh region (no address is rewritten in the kernel), so
+// no L2 can hold an older copy of a line it reads. The relay is one fresh
+// 64-B slot per round for the same reason. Active blocks per round are
+// min(gridDim, ceil(8h / kBlock)), non-increasing, so a block that is idle
+// in a round exits; every wait gives up after ~1 s like block_get_r.
+// ---------------------------------------------------------------------------
+struct TailArgs {
+  const Fe* in[4];    // tables of the round before the first tail round (4 h0 elements each)
+  Fe* out;            // fresh regions: round m writes 4 tables of 2 (h0 >> m) at out + 8 (h0 - (h0 >> m))
+  uint64_t h0;        // pairs in the first tail round
+  uint32_t nrounds;   // tail rounds
+  uint32_t rtag0;     // challenge tag awaited by round 0
+  const RWait* host;  // pinned challenge slot
+  RWait* relay;       // nrounds fresh 64-B relay slots
+  uint32_t* err;      // pinned error word
+  uint64_t* trace;    // debug (ZK_DEBUG_TAIL): per round 8 s_memrealtime stamps, or null
+};
+#define ZK_TAIL_STAMP(m, i) \
+  do { if (a.trace) a.trace[(m) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+
+__device__ __forceinline__ Fe ld_fe_a(const Fe* p, uint64_t i) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p + i);
+  Fe r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t w = __hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.v[2 * k] = (uint32_t)w;
+    r.v[2 * k + 1] = (uint32_t)(w >> 32);
+  }
+  return r;
+}
+__device__ __forceinline__ void st_fe_a(Fe* p, uint64_t i, const Fe& x) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p + i);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    __hip_atomic_store(q + k, (uint64_t)x.v[2 * k] | ((uint64_t)x.v[2 * k + 1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__host__ __device__ __forceinline__ uint64_t tail_region(uint64_t h0, uint32_t m) { return 8 * (h0 - (h0 >> m)); }
+
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_gkr_tail(TailArgs a, RoundSink sink) {
+  __shared__ LimbScratch<17> sc;
+  __shared__ Fe s_r;
+  const uint32_t lane = threadIdx.x & 63, s = threadIdx.x & 7, tb = s >> 1, half = s & 1;
+  const bool mine = (s & 2u) == 0;  // s in {0, 1, 4, 5}: the product lanes
+  for (uint32_t m = 0; m < a.nrounds; ++m) {
+    const uint64_t h = a.h0 >> m;
+    const uint64_t want = (8 * h + kBlock - 1) / kBlock;
+    const uint32_t nb = want < gridDim.x ? (uint32_t)want : gridDim.x;
+    if (blockIdx.x >= nb) return;  // idle from here on (nb never grows)
+    // ---- challenge r_{k-1}: block 0 polls the host, the others its relay ----
+    if (threadIdx.x == 0) {
+      if (blockIdx.x == 0) ZK_TAIL_STAMP(m, 0);
+      const uint32_t tag = a.rtag0 + m;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool ok = true;
+      Fe r;
+      if (blockIdx.x == 0) {
+        while ((int32_t)(__hip_atomic_load(&a.host->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - tag) < 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = false; break; }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = __hip_atomic_load(&a.host->r.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (nb > 1) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            __hip_atomic_store(&a.relay[m].r.v[i], r.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(&a.relay[m].tag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        const RWait* rl = a.relay + m;
+        while ((int32_t)(__hip_atomic_load(&rl->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tag) < 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = false; break; }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = __hip_atomic_load(&rl->r.v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (!ok) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_r = r;
+      if (blockIdx.x == 0) ZK_TAIL_STAMP(m, 1);
+    }
+    __syncthreads();
+    const Fe r = s_r;
+    // ---- fold by r and evaluate e0, e2 (the k_gkr_round_lanes step) ----
+    const Fe* X;
+    if (m == 0) {
+      X = a.in[tb];
+    } else {
+      X = a.out + tail_region(a.h0, m - 1) + (uint64_t)tb * 4 * h;  // previous round: 4 tables of 4h
+    }
+    Fe* Y = a.out + tail_region(a.h0, m) + (uint64_t)tb * 2 * h;
+    Wide acc = wide_zero<F>();
+    const uint64_t stride = (uint64_t)nb * (kBlock / 8);
+    for (uint64_t j = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 3; j < h; j += stride) {
+      const uint64_t o = j + half * h;
+      const Fe f = fold1<F>(ld_fe_a(X, o), ld_fe_a(X, o + 2 * h), r);
+      st_fe_a(Y, o, f);
+      const Fe lo = shfl_fe(f, (int)(lane & ~1u));
+      const Fe v = half ? at2<F>(lo, f) : f;
+      const Fe partner = shfl_fe(v, (int)((lane + 2) & 63));
+      wide_mac<F>(acc, v, partner);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores have landed
+    if (blockIdx.x == 0 && threadIdx.x == 0) ZK_TAIL_STAMP(m, 2);
+    const Wide z = wide_zero<F>();
+    block_limb_sums(mine && half == 0 ? acc : z, sc, 0);
+    block_limb_sums(mine && half == 1 ? acc : z, sc, 17);
+    __syncthreads();
+    // ---- fan-in over the nb active blocks, publish ----
+    RoundSink sk = sink;
+    sk.tag = sink.tag + m;
+    const uint32_t t = threadIdx.x;
+    if (nb > 1) {
+      if (t < 34u) __hip_atomic_fetch_add(sk.accum + t, sc.tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sc.am_last = prev == nb - 1;
+      }
+      __syncthreads();
+      if (sc.am_last) {
+        if (t == 0) ZK_TAIL_STAMP(m, 3);
+        if (t < 34u) sc.tot[t] = __hip_atomic_exchange(sk.accum + t, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publish_limbs<34>(sc, sk);
+        if (t == 0) ZK_TAIL_STAMP(m, 4);
+      }
+    } else {
+      if (t == 0) ZK_TAIL_STAMP(m, 3);
+      publish_limbs<34>(sc, sk);
+      if (t == 0) ZK_TAIL_STAMP(m, 4);
+    }
+    __syncthreads();  // sc and s_r are reused next round
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Two rounds per kernel ("double round"). Round m's fold tables are never
+// materialised: the kernel applies the NP pending challenges of the previous
+// step (NP = 2: r_{m-2}, r_{m-1} by one fold2 per output; NP = 1: r_{m-1})
+// to the input tables (size 4 NP Q) and writes the level-m tables Z (size 4Q,
+// index bit 2Q = variable m, bit Q = variable m+1). On Z it accumulates
+//   round m:   e0 = sum Z(x_m = 0) products, e2 = sum X(2) products
+//              (sum_check_protocol.rs:152-166 on the folded tables), and
+//   round m+1: the sums at t = 0 and t = 2 as quadratics in the still-unknown
+//              r_m. With q_k = Z[j + kQ] (k = 0..3) of a quad j < Q, folding by
+//              r gives lo = (1-r) q0 + r q2, hi = (1-r) q1 + r q3, so
+//              A'(0) = (1-r) q0 + r q2 and A'(2) = (1-r) w0 + r w1 with
+//              w0 = 2 q1 - q0, w1 = 2 q3 - q2; a product sum over (1-r) u + r v
+//              is (1-r)^2 Suu + r(1-r) (S(u+v)(u+v) - Suu - Svv) + r^2 Svv.
+// Eight product sums, all of values in [0, p) (limb sums, exact), category c:
+//   0 alpha  = q0 q0        1 rho  = (q0+q2)(q0+q2)   2 delta = q1 q1
+//   3 e2     = (2q2-q0)^2 + (2q3-q1)^2               4 kappa = q2 q2
+//   5 W00    = w0 w0        6 W11  = w1 w1            7 Wrho  = (w0+w1)(w0+w1)
+// ("x^2" = the A-side value times the S-side value, plus M times P). The host
+// finishes round m (e0 = alpha + delta), draws r_m, evaluates the round m+1
+// quadratics at r_m, draws r_{m+1} and posts (r_m, r_{m+1}, r_m r_{m+1}):
+// one hand-off and one kernel per two rounds, and the level-(m+1) tables are
+// never written.
+//
+// Layout: wave w of a block computes the quarter q_w of 32 quads for both
+// tables of one product (lanes 0-31: A,S; 32-63: M,P) and stores it; the
+// quarters meet in LDS and wave w then forms the products of category 2w and
+// 2w+1 (wave-uniform roles, no divergence).
+//
+// Challenges arrive as 24 self-tagged words (tag << 32 | limb of ra, rb, rab):
+// one load per lane polls and reads them at once, block 0 relays the same
+// words; a word is valid when its tag is >= the awaited one, so no ordering
+// between the words is needed.
+// ---------------------------------------------------------------------------
+struct alignas(64) RPost {
+  uint64_t w[24];
+  uint64_t pad[8];
+};
+struct DIn {
+  Fe ra, rb, rab;      // used as is when host == null
+  const RPost* host;   // pinned slot the host posts to, or null
+  RPost* relay;        // device relay slot (used when gridDim > 1)
+  uint32_t* err;       // pinned error word
+  uint32_t tag;
+};
+__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab) {
+  if (!in.host) {
+    ra = in.ra;
+    rb = in.rb;
+    rab = in.rab;
+    return;
+  }
+  __shared__ uint32_t s_w[24];
+  if (threadIdx.x < 64) {  // wave 0
+    const uint32_t lane = threadIdx.x;
+    const bool mine = lane < 24;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const bool direct = blockIdx.x == 0;
+    uint64_t v = 0;
+    bool ok = true;
+    while (true) {
+      if (mine)
+        v = direct ? __hip_atomic_load(&in.host->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                   : __hip_atomic_load(&in.relay->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool ready = !mine || (int32_t)((uint32_t)(v >> 32) - in.tag) >= 0;
+      if (__all(ready)) break;
+      if (direct) __builtin_amdgcn_s_sleep(2); else __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = false; break; }
+    }
+    if (direct && gridDim.x > 1 && mine) __hip_atomic_store(&in.relay->w[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!ok && lane == 0) __hip_atomic_store(in.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (mine) s_w[lane] = (uint32_t)v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ra.v[i] = s_w[i];
+    rb.v[i] = s_w[8 + i];
+    rab.v[i] = s_w[16 + i];
+  }
+}
+
+constexpr int kDCats = 8;             // product-sum categories of a double round
+constexpr int kDLimbs = kDCats * 17;  // 136 limb sums
+struct DScratch {
+  union {
+    uint32_t qs[4 * 2 * 2 * 8 * 32];  // [quarter][product][table][word][quad]
+    uint32_t rows[4 * 64 * 35];       // per-wave limb-sum transpose (odd stride)
+  };
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+};
+__device__ __forceinline__ uint32_t dq_idx(uint32_t k, uint32_t pp, uint32_t tab, uint32_t w, uint32_t jl) {
+  return (((k * 2 + pp) * 2 + tab) * 8 + w) * 32 + jl;
+}
+
+template <class F, int NP>
+__global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
+                                                       Fe* __restrict__ A2, Fe* __restrict__ S2,
+                                                       Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t Q,
+                                                       DIn din, RoundSink sink) {
+  static_assert(NP == 1 || NP == 2, "one or two pending challenges");
+  Fe ra, rb, rab;
+  block_get_rs(din, ra, rb, rab);
+  __shared__ DScratch sc;
+  const uint32_t lane = threadIdx.x & 63, role = threadIdx.x >> 6, jl = lane & 31, pp = lane >> 5;
+  const Fe* __restrict__ X = pp ? M : A;
+  const Fe* __restrict__ Y = pp ? P : S;
+  Fe* __restrict__ X2 = pp ? M2 : A2;
+  Fe* __restrict__ Y2 = pp ? P2 : S2;
+  const uint64_t h4 = 4 * Q;
+  Wide acc0 = wide_zero<F>(), acc1 = wide_zero<F>();
+  for (uint64_t jb = (uint64_t)blockIdx.x * 32; jb < Q; jb += (uint64_t)gridDim.x * 32) {
+    const uint64_t j = jb + jl;
+    const bool act = j < Q;
+    Fe zx = fe_zero<F>(), zy = fe_zero<F>();
+    if (act) {
+      const uint64_t i = j + role * Q;
+      if (NP == 2) {
+        const Fe x00 = ld_fe(X, i), x01 = ld_fe(X, i + h4), x10 = ld_fe(X, i + 2 * h4), x11 = ld_fe(X, i + 3 * h4);
+        const Fe y00 = ld_fe(Y, i), y01 = ld_fe(Y, i + h4), y10 = ld_fe(Y, i + 2 * h4), y11 = ld_fe(Y, i + 3 * h4);
+        __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
+        zx = fold2<F>(x00, x01, x10, x11, ra, rb, rab);
+        zy = fold2<F>(y00, y01, y10, y11, ra, rb, rab);
+      } else {
+        const Fe x0 = ld_fe(X, i), x1 = ld_fe(X, i + h4), y0 = ld_fe(Y, i), y1 = ld_fe(Y, i + h4);
+        __builtin_amdgcn_sched_barrier(0);
+        zx = fold1<F>(x0, x1, rb);
+        zy = fold1<F>(y0, y1, rb);
+      }
+      st_fold(X2, i, zx);
+      st_fold(Y2, i, zy);
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      sc.qs[dq_idx(role, pp, 0, w, jl)] = zx.v[w];
+      sc.qs[dq_idx(role, pp, 1, w, jl)] = zy.v[w];
+    }
+    __syncthreads();
+    if (act) {
+      auto q = [&](uint32_t k, uint32_t tab) {
+        Fe r;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) r.v[w] = sc.qs[dq_idx(k, pp, tab, w, jl)];
+        return r;
+      };
+      if (role == 0) {  // alpha = q0 q0, rho = (q0 + q2)^2
+        const Fe q2x = q(2, 0), q2y = q(2, 1);
+        wide_mac<F>(acc0, zx, zy);
+        wide_mac<F>(acc1, fe_add<F>(zx, q2x), fe_add<F>(zy, q2y));
+      } else if (role == 1) {  // delta = q1 q1, e2 = (2q2 - q0)^2 + (2q3 - q1)^2
+        const Fe q0x = q(0, 0), q0y = q(0, 1), q2x = q(2, 0), q2y = q(2, 1), q3x = q(3, 0), q3y = q(3, 1);
+        wide_mac<F>(acc0, zx, zy);
+        wide_mac<F>(acc1, at2<F>(q0x, q2x), at2<F>(q0y, q2y));
+        wide_mac<F>(acc1, at2<F>(zx, q3x), at2<F>(zy, q3y));
+      } else if (role == 2) {  // kappa = q2 q2, W00 = w0 w0
+        const Fe q0x = q(0, 0), q0y = q(0, 1), q1x = q(1, 0), q1y = q(1, 1);
+        wide_mac<F>(acc0, zx, zy);
+        wide_mac<F>(acc1, at2<F>(q0x, q1x), at2<F>(q0y, q1y));
+      } else {  // W11 = w1 w1, Wrho = (w0 + w1)^2
+        const Fe q0x = q(0, 0), q0y = q(0, 1), q1x = q(1, 0), q1y = q(1, 1), q2x = q(2, 0), q2y = q(2, 1);
+        const Fe w1x = at2<F>(q2x, zx), w1y = at2<F>(q2y, zy);
+        wide_mac<F>(acc0, w1x, w1y);
+        wide_mac<F>(acc1, fe_add<F>(at2<F>(q0x, q1x), w1x), fe_add<F>(at2<F>(q0y, q1y), w1y));
+      }
+    }
+    __syncthreads();  // qs is rewritten by the next iteration
+  }
+  // per-wave column sums: wave w's (acc0, acc1) -> tot[34 w + 17 s + word]
+  uint32_t* rows = sc.rows + role * 64 * 35;
+#pragma unroll
+  for (int w = 0; w < 17; ++w) {
+    rows[lane * 35 + w] = acc0.w[w];
+    rows[lane * 35 + 17 + w] = acc1.w[w];
+  }
+  __syncthreads();
+  if (lane < 34) {
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll 8
+    for (int r = 0; r < 64; r += 2) {
+      s0 += rows[r * 35 + lane];
+      s1 += rows[(r + 1) * 35 + lane];
+    }
+    sc.tot[role * 34 + lane] = s0 + s1;
+  }
+  __syncthreads();
+  grid_finish<kDLimbs>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------

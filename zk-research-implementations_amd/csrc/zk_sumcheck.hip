@@ -44,14 +44,21 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_LANES_MAX_PAIRS")) c->lanes_max_pairs = strtoull(e, nullptr, 0);  // tuning knob
     if (const char* e = getenv("ZK_FORCE_COLLECTIVES")) c->force_coll = atoi(e) != 0;
     if (const char* e = getenv("ZK_PRELAUNCH")) c->prelaunch = atoi(e) != 0;
+    if (const char* e = getenv("ZK_TAIL")) c->tail = atoi(e) != 0;
+    if (const char* e = getenv("ZK_DROUND")) c->dround = atoi(e) != 0;
+    if (const char* e = getenv("ZK_TAIL_MAX_PAIRS")) c->tail_max_pairs = strtoull(e, nullptr, 0);
     c->num_cus = prop.multiProcessorCount;
     try {
       bind(c);
       HIPCK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
       c->small.ensure(kSmallBytes);
       HIPCK(hipMemset(c->small.p, 0, kSmallBytes));
-      HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), 4096, hipHostMallocMapped | hipHostMallocCoherent));
-      memset(c->h_red, 0, 4096);
+      HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), kHostPage, hipHostMallocMapped | hipHostMallocCoherent));
+      memset(c->h_red, 0, kHostPage);
+      if (getenv("ZK_DEBUG_TAIL")) {
+        HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->tail_trace), 64 * 8 * 8, hipHostMallocMapped | hipHostMallocCoherent));
+        memset(c->tail_trace, 0, 64 * 8 * 8);
+      }
     } catch (...) {
       zk_ctx_destroy(c);
       throw;
@@ -74,6 +81,8 @@ void zk_ctx_destroy(zk_ctx* c) {
   c->work[1].release();
   c->input.release();
   c->partials.release();
+  c->tailbuf.release();
+  if (c->tail_trace) (void)hipHostFree(c->tail_trace);
   c->small.release();
   for (auto& b : c->msm) b.release();
   for (auto& b : c->scan_tmp) b.release();

@@ -17,7 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes"]
+KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround"]
 
 
 class ZkError(RuntimeError):
@@ -28,10 +28,10 @@ class ZkError(RuntimeError):
 
 class ZkStats(C.Structure):
     _fields_ = [
-        ("launches", C.c_uint64 * 10),
-        ("kernel_ms", C.c_double * 10),
-        ("alg_bytes", C.c_double * 10),
-        ("field_muls", C.c_double * 10),
+        ("launches", C.c_uint64 * len(KERNEL_KINDS)),
+        ("kernel_ms", C.c_double * len(KERNEL_KINDS)),
+        ("alg_bytes", C.c_double * len(KERNEL_KINDS)),
+        ("field_muls", C.c_double * len(KERNEL_KINDS)),
         ("host_syncs", C.c_uint64),
         ("collectives", C.c_uint64),
         ("host_wait_us", C.c_double),
