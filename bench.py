@@ -338,7 +338,7 @@ def main() -> None:
             # during the LAST timed step only: their marker packets cost the GPU
             # ~5 us per round, so timing every step would inflate ms_per_step
             st0 = ctx.stats()
-            ctx.set_timing_kinds([] if args.no_events else ["gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround"])
+            ctx.set_timing_kinds([] if args.no_events else ["gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail"])
         step()
     torch.cuda.synchronize()
     barrier()

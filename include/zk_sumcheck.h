@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 6u
+#define ZK_ABI_VERSION 7u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -80,7 +80,8 @@ enum {
   ZK_K_GKR_LANES = 9,  /* the same round for small tables, 8 lanes per pair (k_gkr_round_lanes) */
   ZK_K_GKR_TAIL = 10,  /* the small rounds of a proof in one persistent kernel (k_gkr_tail, ZK_DROUND=0) */
   ZK_K_GKR_DROUND = 11, /* two rounds per kernel: pending folds + round sums + next round's quadratics (k_gkr_dround) */
-  ZK_K_KINDS = 12
+  ZK_K_GKR_DTAIL = 12, /* the small double rounds in one persistent kernel (k_gkr_dtail) */
+  ZK_K_KINDS = 13
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];

@@ -299,13 +299,14 @@ def test_stats_and_timing(ctx):
     ctx.set_timing(False)
     st = ctx.stats()
     k = st["kernels"]
-    # round 0, round 1 alone, then rounds (2,3) .. (10,11) two per kernel
-    assert k["gkr_round0"]["launches"] == 1 and k["gkr_dround"]["launches"] == (n - 2) // 2
+    # round 0, round 1 alone, then rounds (2,3) .. (10,11) two per step; these
+    # small double steps run in one persistent kernel (k_gkr_dtail)
+    assert k["gkr_round0"]["launches"] == 1 and k["gkr_dtail"]["launches"] == 1 and k["gkr_dround"]["launches"] == 0
     assert k["gkr_round"]["launches"] + k["gkr_round_lanes"]["launches"] == 1
     # first double: 1 pending challenge (level 1 -> 2), then 2 pending
     q = [1 << (n - 4 - 2 * d) for d in range((n - 2) // 2)]  # quads of each double step (Z = 4Q)
-    assert k["gkr_dround"]["alg_bytes"] == 1536 * q[0] + 2560 * sum(q[1:])
-    assert k["gkr_dround"]["ms"] > 0 and st["host_syncs"] >= 2 + (n - 2) // 2
+    assert k["gkr_dtail"]["alg_bytes"] == 1536 * q[0] + 2560 * sum(q[1:])
+    assert k["gkr_dtail"]["ms"] > 0 and st["host_syncs"] >= 2 + (n - 2) // 2
     assert k["gkr_round0"]["alg_bytes"] == 256 * (1 << (n - 1))
 
 

@@ -6,6 +6,10 @@
 * From round 2 on two rounds run per kernel (k_gkr_dround, default); the
   proof is identical with one round per kernel (ZK_DROUND=0), for odd and
   even round counts, pre-enqueued or not.
+* The small double steps run in one persistent kernel (k_gkr_dtail, default);
+  the proof is identical with one launch per step (ZK_DTAIL=0), when it
+  starts at the first double step over large tables (ZK_DTAIL_MAX_QUADS) and
+  with one block (ZK_DTAIL_BLOCKS=1).
 * With ZK_DROUND=0 the small rounds run in one persistent kernel (k_gkr_tail);
   the proof is identical with one launch per round (ZK_TAIL=0) and when the
   tail starts at round 1 over large tables (ZK_LANES_MAX_PAIRS).
@@ -112,6 +116,22 @@ def test_double_and_single_rounds_agree_20var(monkeypatch, field):
         finally:
             ctx.close()
     assert got["1"] == got["0"]
+
+
+@pytest.mark.parametrize("field", [0, 2])
+@pytest.mark.parametrize("env", [{"ZK_DTAIL": "0"}, {"ZK_DTAIL_MAX_QUADS": str(1 << 16)}, {"ZK_DTAIL_BLOCKS": "1"},
+                                 {"ZK_DTAIL_MAX_QUADS": "16"}])
+def test_dtail_modes_agree(monkeypatch, field, env):
+    n = 17
+    want = _oracle(field, n)
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    ctx = zk_amd.Context(0)
+    try:
+        assert _prove(ctx, field, n) == want
+        assert _prove(ctx, field, n) == want  # reused tail buffer and relay slots
+    finally:
+        ctx.close()
 
 
 def test_host_failure_mid_proof_releases_waiting_rounds(monkeypatch):

@@ -203,6 +203,9 @@ struct zk_ctx {
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
+  bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
+  uint64_t dtail_max_quads = 1u << 12;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
+  uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
   bool tail = true;         // (ZK_DROUND=0 only) pre-enqueued small rounds in one persistent kernel (ZK_TAIL=0: one launch each)
   uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
   uint64_t* tail_trace = nullptr;      // ZK_DEBUG_TAIL: pinned per-round stamps of the tail kernel, printed per proof
@@ -496,15 +499,16 @@ inline bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1; }
 inline bool use_tail(zk_ctx* c, bool across_ranks) {
   return c->tail && !(across_ranks && multi_rank(c) && c->comm == COMM_RCCL);
 }
-constexpr size_t kTailRelayBytes = 64 * sizeof(zk::RWait);
+constexpr size_t kTailRelayBytes = 64 * sizeof(zk::RPost);  // 64 relay slots (k_gkr_tail: RWait, k_gkr_dtail: RPost)
 inline size_t tail_bytes(uint64_t h0) { return kTailRelayBytes + 16 * h0 * sizeof(Fe); }
 
 struct GStep {
-  int kind;    // 0 round 0, 1 single, 2 double, 3 tail
-  uint32_t i;  // first round (local)
-  int np;      // double: pending challenges at entry (1 or 2)
+  int kind;        // GS_*
+  uint32_t i;      // first round (local)
+  int np;          // double / dtail: pending challenges at entry (1 or 2)
+  uint32_t nd = 0; // dtail: double steps it runs
 };
-enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3 };
+enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4 };
 
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
@@ -518,6 +522,21 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
     if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
     for (int np = 1; i + 1 < nv; i += 2, np = 2) steps.push_back({GS_DOUBLE, i, np});
+    // the small doubles (>= 2 of them) in one persistent kernel
+    if (pre && c->dtail && use_tail(c, across_ranks)) {
+      size_t d0 = 0;
+      while (d0 < steps.size() && !(steps[d0].kind == GS_DOUBLE && (L >> steps[d0].i) / 4 <= c->dtail_max_quads)) ++d0;
+      const size_t nd = steps.size() - d0;
+      if (d0 < steps.size() && nd >= 2 && nd <= 64) {
+        const GStep first = steps[d0];
+        steps.resize(d0);
+        steps.push_back({GS_DTAIL, first.i, first.np, (uint32_t)nd});
+        const uint64_t Q0 = (L >> first.i) / 4;
+        const size_t had = c->tailbuf.bytes;
+        c->tailbuf.ensure(kTailRelayBytes + zk::dtail_region(Q0, (uint32_t)nd) * sizeof(Fe));
+        if (c->tailbuf.bytes != had) HIPCK(hipMemset(c->tailbuf.p, 0, kTailRelayBytes));  // relay tags at rest
+      }
+    }
   } else {
     // first round >= 1 with <= tail_max_pairs pairs, if at least two rounds remain
     uint32_t tail0 = nv;
@@ -589,6 +608,35 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       for (int t = 0; t < 4; ++t) cur[t] = last + (uint64_t)t * 2 * hl;
       return;
     }
+    if (st.kind == GS_DTAIL) {
+      const uint64_t Q0 = size / 4;
+      for (uint32_t d = 1; d < st.nd; ++d) sinks[i + 2 * d] = make_sink(c, across_ranks);
+      zk::DTailArgs a{};
+      for (int t = 0; t < 4; ++t) a.in[t] = cur[t];
+      a.relay = reinterpret_cast<zk::RPost*>(c->tailbuf.p);
+      a.out = reinterpret_cast<Fe*>(reinterpret_cast<char*>(c->tailbuf.p) + kTailRelayBytes);
+      a.Q0 = Q0;
+      a.nsteps = st.nd;
+      a.np0 = (uint32_t)st.np;
+      a.host = h_rpost(c);
+      a.err = h_err(c);
+      rtags[si] = c->rtag + 1;
+      c->rtag += st.nd;
+      a.rtag0 = rtags[si];
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(
+          {(Q0 + 31) / 32, (uint64_t)std::min<uint32_t>(c->dtail_blocks, 64u), (uint64_t)c->num_cus});
+      double bytes = 0, muls = 0;
+      for (uint32_t d = 0; d < st.nd; ++d) {
+        const bool two = d > 0 || st.np == 2;
+        bytes += (two ? 2560.0 : 1536.0) * (Q0 >> (2 * d));
+        muls += (two ? 40.0 : 24.0) * (Q0 >> (2 * d));
+      }
+      launch(c, ZK_K_GKR_DTAIL, bytes, muls, zk::k_gkr_dtail<F>, std::max<uint32_t>(grid, 1u), a, sk);
+      const uint64_t Ql = Q0 >> (2 * (st.nd - 1));
+      Fe* last = a.out + zk::dtail_region(Q0, st.nd - 1);
+      for (int t = 0; t < 4; ++t) cur[t] = last + (uint64_t)t * 4 * Ql;
+      return;
+    }
     if (st.kind == GS_DOUBLE) {
       // input: level i - np (size << np), output Z: level i (size = 4Q)
       const uint64_t Q = size / 4;
@@ -608,7 +656,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.rb = rb;
       }
       const uint32_t grid = grid_for(c, 8 * Q, zk::k_gkr_dround<F, 2>);
-      const double bytes = (st.np == 2 ? 2560.0 : 1536.0) * Q, muls = (st.np == 2 ? 41.0 : 25.0) * Q;
+      const double bytes = (st.np == 2 ? 2560.0 : 1536.0) * Q, muls = (st.np == 2 ? 40.0 : 24.0) * Q;
       if (st.np == 2)
         launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dround<F, 2>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
                nx[1], nx[2], nx[3], Q, din, sk);
@@ -643,7 +691,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   };
   // the highest challenge tag step si (and every step before it) waits for
   auto last_tag = [&](size_t si) {
-    return steps[si].kind == GS_TAIL ? rtags[si] + (nv - steps[si].i) - 1 : rtags[si];
+    if (steps[si].kind == GS_TAIL) return rtags[si] + (nv - steps[si].i) - 1;
+    if (steps[si].kind == GS_DTAIL) return rtags[si] + steps[si].nd - 1;
+    return rtags[si];
   };
   PostR post{c};
   if (pre) {
@@ -660,7 +710,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   auto hand_on = [&](size_t si) {
     if (!pre || si + 1 >= ns) return;
     const GStep& nx = steps[si + 1];
-    if (nx.kind == GS_DOUBLE) {
+    if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
       if (nx.np == 2)
         post.post2(ra, rb, zk::fe_mul<F>(ra, rb), rtags[si + 1]);
       else
@@ -673,6 +723,26 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     claim = finish_round<F>(tr, e0, e1, e2, k0 + i, out, r);
     ra = rb;
     rb = r;
+  };
+  // rounds i0 and i0 + 1 from a double step's eight product sums
+  auto two_rounds = [&](uint32_t i0) {
+      Fe d[zk::kDCats];
+      collect_sums<F, zk::kDCats>(c, sinks[i0], across_ranks, 17, d);
+      // categories: 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21, 7 V12 (kernels.hpp)
+      // round i: e0 = V00 + V01, e2 = V20 + V21
+      const Fe e0 = zk::fe_add<F>(d[0], d[2]);
+      one_round(i0, e0, zk::fe_sub<F>(claim, e0), zk::fe_add<F>(d[5], d[6]));
+      // round i + 1 at r = r_i: e0' through (V00, V10, V20), e2' through (V02, V12, V22) at r = 0, 1, 2
+      const Fe one = zk::fe_one<F>(), two = zk::fe_add<F>(one, one), h = zk::fe_inv2<F>();
+      const Fe rm1 = zk::fe_sub<F>(r, one), rm2 = zk::fe_sub<F>(r, two);
+      const Fe L0 = zk::fe_mul<F>(zk::fe_mul<F>(rm1, rm2), h);                 // (r-1)(r-2)/2
+      const Fe L1 = zk::fe_sub<F>(zk::fe_zero<F>(), zk::fe_mul<F>(r, rm2));     // -r(r-2)
+      const Fe L2 = zk::fe_mul<F>(zk::fe_mul<F>(r, rm1), h);                   // r(r-1)/2
+      auto lag = [&](const Fe& v0, const Fe& v1, const Fe& v2) {
+        return zk::fe_add<F>(zk::fe_add<F>(zk::fe_mul<F>(L0, v0), zk::fe_mul<F>(L1, v1)), zk::fe_mul<F>(L2, v2));
+      };
+      const Fe f0 = lag(d[0], d[4], d[5]), f2 = lag(d[3], d[7], d[1]);
+      one_round(i0 + 1, f0, zk::fe_sub<F>(claim, f0), f2);
   };
   for (size_t si = 0; si < ns; ++si) {
     const GStep& st = steps[si];
@@ -695,21 +765,14 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         if (pre && i + 1 < nv) post.post(r, rtags[si] + (i + 1 - st.i));
       }
       pend = 1;
-    } else {
-      Fe d[zk::kDCats];
-      collect_sums<F, zk::kDCats>(c, sinks[st.i], across_ranks, 17, d);
-      // round i on Z: e0 = alpha + delta, e2
-      const Fe e0 = zk::fe_add<F>(d[0], d[2]);
-      one_round(st.i, e0, zk::fe_sub<F>(claim, e0), d[3]);
-      // round i + 1: sum over (1-r) u + r v = (1-r)^2 Suu + r(1-r)(S(u+v)^2 - Suu - Svv) + r^2 Svv
-      const Fe one = zk::fe_one<F>(), omr = zk::fe_sub<F>(one, r);
-      const Fe c00 = zk::fe_mul<F>(omr, omr), c01 = zk::fe_mul<F>(r, omr), c11 = zk::fe_mul<F>(r, r);
-      auto quad = [&](const Fe& suu, const Fe& suv2, const Fe& svv) {
-        const Fe cross = zk::fe_sub<F>(zk::fe_sub<F>(suv2, suu), svv);
-        return zk::fe_add<F>(zk::fe_add<F>(zk::fe_mul<F>(c00, suu), zk::fe_mul<F>(c01, cross)), zk::fe_mul<F>(c11, svv));
-      };
-      const Fe f0 = quad(d[0], d[1], d[4]), f2 = quad(d[5], d[7], d[6]);
-      one_round(st.i + 1, f0, zk::fe_sub<F>(claim, f0), f2);
+    } else if (st.kind == GS_DOUBLE) {
+      two_rounds(st.i);
+      pend = 2;
+    } else {  // GS_DTAIL
+      for (uint32_t d = 0; d < st.nd; ++d) {
+        two_rounds(st.i + 2 * d);
+        if (d + 1 < st.nd) post.post2(ra, rb, zk::fe_mul<F>(ra, rb), rtags[si] + d + 1);
+      }
       pend = 2;
     }
     hand_on(si);

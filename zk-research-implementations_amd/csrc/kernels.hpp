@@ -679,33 +679,29 @@ __global__ __launch_bounds__(kBlock) void k_gkr_tail(TailArgs a, RoundSink sink)
 }
 
 // ---------------------------------------------------------------------------
-// Two rounds per kernel ("double round"). Round m's fold tables are never
-// materialised: the kernel applies the NP pending challenges of the previous
-// step (NP = 2: r_{m-2}, r_{m-1} by one fold2 per output; NP = 1: r_{m-1})
-// to the input tables (size 4 NP Q) and writes the level-m tables Z (size 4Q,
-// index bit 2Q = variable m, bit Q = variable m+1). On Z it accumulates
-//   round m:   e0 = sum Z(x_m = 0) products, e2 = sum X(2) products
-//              (sum_check_protocol.rs:152-166 on the folded tables), and
-//   round m+1: the sums at t = 0 and t = 2 as quadratics in the still-unknown
-//              r_m. With q_k = Z[j + kQ] (k = 0..3) of a quad j < Q, folding by
-//              r gives lo = (1-r) q0 + r q2, hi = (1-r) q1 + r q3, so
-//              A'(0) = (1-r) q0 + r q2 and A'(2) = (1-r) w0 + r w1 with
-//              w0 = 2 q1 - q0, w1 = 2 q3 - q2; a product sum over (1-r) u + r v
-//              is (1-r)^2 Suu + r(1-r) (S(u+v)(u+v) - Suu - Svv) + r^2 Svv.
-// Eight product sums, all of values in [0, p) (limb sums, exact), category c:
-//   0 alpha  = q0 q0        1 rho  = (q0+q2)(q0+q2)   2 delta = q1 q1
-//   3 e2     = (2q2-q0)^2 + (2q3-q1)^2               4 kappa = q2 q2
-//   5 W00    = w0 w0        6 W11  = w1 w1            7 Wrho  = (w0+w1)(w0+w1)
-// ("x^2" = the A-side value times the S-side value, plus M times P). The host
-// finishes round m (e0 = alpha + delta), draws r_m, evaluates the round m+1
-// quadratics at r_m, draws r_{m+1} and posts (r_m, r_{m+1}, r_m r_{m+1}):
-// one hand-off and one kernel per two rounds, and the level-(m+1) tables are
-// never written.
-//
-// Layout: wave w of a block computes the quarter q_w of 32 quads for both
-// tables of one product (lanes 0-31: A,S; 32-63: M,P) and stores it; the
-// quarters meet in LDS and wave w then forms the products of category 2w and
-// 2w+1 (wave-uniform roles, no divergence).
+// Two rounds per kernel ("double round"). The tables of every other level are
+// never materialised: the kernel applies the NP pending challenges of the
+// previous step (NP = 2: r_{m-2}, r_{m-1} by one fold2 per output; NP = 1:
+// r_{m-1}) to the input tables (size 4 NP Q) and writes the level-m tables Z
+// (size 4Q: index bit 2Q = variable m, bit Q = variable m+1). A quad j < Q
+// holds the corners V(a,b) = Z[j + (2a + b) Q] of a bilinear function of
+// (x_m, x_{m+1}); extended to a, b in {0,1,2} (V(2,b) = 2V(1,b) - V(0,b),
+// V(a,2) = 2V(a,1) - V(a,0)) it gives every value either round needs:
+//   round m:    e0 = sum V(0,0)^2 + V(0,1)^2,  e2 = sum V(2,0)^2 + V(2,1)^2
+//               (sum_check_protocol.rs:152-166 on the folded tables);
+//   round m+1:  with r_m still unknown, folding by r gives lo = V(r,0),
+//               X(2) = V(r,2), so e0'(r) and e2'(r) are quadratics in r given
+//               by their values at r = 0, 1, 2: V(.,0)^2 and V(.,2)^2.
+// ("V^2" = the A-side value times the S-side value, plus M times P.) That is
+// the 3x3 grid without its centre: 8 product sums, two per lane. Lane k of
+// the 4 lanes of a quad holds corner k and forms, by quad_perm DPP moves
+// (no LDS, no barrier), the extended point it multiplies:
+//   k = 0 (0,0): V(0,0), V(2,2)     k = 1 (0,1): V(0,1), V(0,2)
+//   k = 2 (1,0): V(1,0), V(2,0)     k = 3 (1,1): V(2,1), V(1,2)
+// Category c = 2k + slot: 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21,
+// 7 V12 (limb sums of values in [0, p): exact). The host finishes round m,
+// draws r_m, interpolates round m+1's values at r_m, draws r_{m+1} and posts
+// (r_m, r_{m+1}, r_m r_{m+1}): one hand-off and one kernel per two rounds.
 //
 // Challenges arrive as 24 self-tagged words (tag << 32 | limb of ra, rb, rab):
 // one load per lane polls and reads them at once, block 0 relays the same
@@ -723,7 +719,7 @@ struct DIn {
   uint32_t* err;       // pinned error word
   uint32_t tag;
 };
-__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab) {
+__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab, bool relay) {
   if (!in.host) {
     ra = in.ra;
     rb = in.rb;
@@ -747,7 +743,7 @@ __device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& 
       if (direct) __builtin_amdgcn_s_sleep(2); else __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitTicks) { ok = false; break; }
     }
-    if (direct && gridDim.x > 1 && mine) __hip_atomic_store(&in.relay->w[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (direct && relay && mine) __hip_atomic_store(&in.relay->w[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!ok && lane == 0) __hip_atomic_store(in.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (mine) s_w[lane] = (uint32_t)v;
   }
@@ -763,16 +759,57 @@ __device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& 
 constexpr int kDCats = 8;             // product-sum categories of a double round
 constexpr int kDLimbs = kDCats * 17;  // 136 limb sums
 struct DScratch {
-  union {
-    uint32_t qs[4 * 2 * 2 * 8 * 32];  // [quarter][product][table][word][quad]
-    uint32_t rows[4 * 64 * 35];       // per-wave limb-sum transpose (odd stride)
-  };
+  uint32_t rows[kBlock * 35];  // limb-sum transpose: 2 x 17 words per thread (odd stride)
   uint64_t tot[kSlotU64];
   uint64_t pp[kBlock];
   uint32_t am_last;
 };
-__device__ __forceinline__ uint32_t dq_idx(uint32_t k, uint32_t pp, uint32_t tab, uint32_t w, uint32_t jl) {
-  return (((k * 2 + pp) * 2 + tab) * 8 + w) * 32 + jl;
+// quad_perm DPP move of a field element: lane 4i + k reads lane 4i + perm[k]
+template <int CTRL>
+__device__ __forceinline__ Fe dpp_fe(const Fe& x) {
+  Fe r;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) r.v[w] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[w], CTRL, 0xF, 0xF, false);
+  return r;
+}
+__device__ __forceinline__ Fe sel_fe(bool c, const Fe& a, const Fe& b) {
+  Fe r;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) r.v[w] = c ? a.v[w] : b.v[w];
+  return r;
+}
+constexpr int kQP0001 = 0x40, kQP3333 = 0xFF, kQP2222 = 0xAA;  // quad_perm [0,0,0,1], [3,3,3,3], [2,2,2,2]
+// corner q of lane k -> (slot 1, slot 2) points (see the table above)
+template <class F>
+__device__ __forceinline__ void grid_points(const Fe& q, uint32_t k, Fe& s1, Fe& s2) {
+  const Fe e1 = at2<F>(dpp_fe<kQP0001>(q), q);  // k=1: V02, k=2: V20, k=3: V21
+  const Fe xa = dpp_fe<kQP3333>(e1), ya = dpp_fe<kQP2222>(e1), yb = dpp_fe<kQP2222>(q);
+  const Fe e2 = at2<F>(sel_fe(k == 0, ya, yb), sel_fe(k == 0, xa, q));  // k=0: V22, k=3: V12
+  s1 = sel_fe(k == 3, e1, q);
+  s2 = sel_fe(k == 0 || k == 3, e2, e1);
+}
+
+// limb sums: category c = 2k + s over the 64 threads of the block with lane & 3 == k
+// -> sc.tot[17 c + word] (valid after the call)
+__device__ __forceinline__ void dround_limb_sums(const Wide& acc0, const Wide& acc1, DScratch& sc) {
+#pragma unroll
+  for (int w = 0; w < 17; ++w) {
+    sc.rows[threadIdx.x * 35 + w] = acc0.w[w];
+    sc.rows[threadIdx.x * 35 + 17 + w] = acc1.w[w];
+  }
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  if (t < (uint32_t)kDLimbs) {
+    const uint32_t c = t / 17, w = t % 17, kk = c >> 1, off = (c & 1) * 17 + w;
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll 8
+    for (uint32_t m = 0; m < 64; m += 2) {
+      s0 += sc.rows[(4 * m + kk) * 35 + off];
+      s1 += sc.rows[(4 * m + 4 + kk) * 35 + off];
+    }
+    sc.tot[t] = s0 + s1;
+  }
+  __syncthreads();
 }
 
 template <class F, int NP>
@@ -783,9 +820,11 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
                                                        DIn din, RoundSink sink) {
   static_assert(NP == 1 || NP == 2, "one or two pending challenges");
   Fe ra, rb, rab;
-  block_get_rs(din, ra, rb, rab);
+  block_get_rs(din, ra, rb, rab, gridDim.x > 1);
   __shared__ DScratch sc;
-  const uint32_t lane = threadIdx.x & 63, role = threadIdx.x >> 6, jl = lane & 31, pp = lane >> 5;
+  // wave w: product w & 1 (A*S or M*P), quads (w >> 1) * 16 + [0, 16) of each 32
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3;
+  const uint32_t pp = wv & 1, jl = (wv >> 1) * 16 + (lane >> 2);
   const Fe* __restrict__ X = pp ? M : A;
   const Fe* __restrict__ Y = pp ? P : S;
   Fe* __restrict__ X2 = pp ? M2 : A2;
@@ -794,10 +833,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
   Wide acc0 = wide_zero<F>(), acc1 = wide_zero<F>();
   for (uint64_t jb = (uint64_t)blockIdx.x * 32; jb < Q; jb += (uint64_t)gridDim.x * 32) {
     const uint64_t j = jb + jl;
-    const bool act = j < Q;
-    Fe zx = fe_zero<F>(), zy = fe_zero<F>();
-    if (act) {
-      const uint64_t i = j + role * Q;
+    if (j < Q) {  // uniform over the 4 lanes of a quad
+      const uint64_t i = j + k * Q;
+      Fe zx, zy;
       if (NP == 2) {
         const Fe x00 = ld_fe(X, i), x01 = ld_fe(X, i + h4), x10 = ld_fe(X, i + 2 * h4), x11 = ld_fe(X, i + 3 * h4);
         const Fe y00 = ld_fe(Y, i), y01 = ld_fe(Y, i + h4), y10 = ld_fe(Y, i + 2 * h4), y11 = ld_fe(Y, i + 3 * h4);
@@ -812,61 +850,126 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
       }
       st_fold(X2, i, zx);
       st_fold(Y2, i, zy);
+      Fe ax, bx, ay, by;
+      grid_points<F>(zx, k, ax, bx);
+      grid_points<F>(zy, k, ay, by);
+      wide_mac<F>(acc0, ax, ay);
+      wide_mac<F>(acc1, bx, by);
     }
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      sc.qs[dq_idx(role, pp, 0, w, jl)] = zx.v[w];
-      sc.qs[dq_idx(role, pp, 1, w, jl)] = zy.v[w];
+  }
+  dround_limb_sums(acc0, acc1, sc);
+  grid_finish<kDLimbs>(sc, sink);
+}
+
+// ---------------------------------------------------------------------------
+// The small double rounds of a proof in ONE persistent kernel: step s is the
+// k_gkr_dround step over Q0 >> 2s quads (two pending challenges, the first
+// step np0), run by min(gridDim, Q/32) blocks. The instruction cache stays
+// warm and no launch sits between steps; per step block 0 waits for the
+// host's three challenges (tag rtag0 + s) and relays them through a fresh
+// slot, the active blocks fold and evaluate, their 136 limb sums meet in the
+// u64 accumulator (<= 64 blocks), and the last block publishes (sink tag
+// tag0 + s). Tables written in step s are read by other blocks in step s+1:
+// every store and load of them is an 8-byte agent-scope atomic (sc1), every
+// storing wave drains before its block counts in, and each step writes a
+// fresh region (MI355X_MICROARCH.md "Valid forms"), as in k_gkr_tail.
+// ---------------------------------------------------------------------------
+struct DTailArgs {
+  const Fe* in[4];    // input tables of step 0 (4 np0 Q0 elements each)
+  Fe* out;            // step s writes 4 tables of 4 (Q0 >> 2s) at out + dtail_region(Q0, s)
+  uint64_t Q0;        // quads of step 0
+  uint32_t nsteps;
+  uint32_t np0;       // pending challenges at step 0 (1 or 2)
+  uint32_t rtag0;     // challenge tag awaited by step 0
+  const RPost* host;  // pinned challenge words
+  RPost* relay;       // nsteps fresh relay slots
+  uint32_t* err;      // pinned error word
+};
+__host__ __device__ __forceinline__ uint64_t dtail_region(uint64_t Q0, uint32_t s) {
+  uint64_t o = 0;
+  for (uint32_t t = 0; t < s; ++t) o += 16 * (Q0 >> (2 * t));
+  return o;
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sink) {
+  __shared__ DScratch sc;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3;
+  const uint32_t pp = wv & 1, jl = (wv >> 1) * 16 + (lane >> 2);
+  for (uint32_t st = 0; st < a.nsteps; ++st) {
+    const uint64_t Q = a.Q0 >> (2 * st);
+    const uint64_t want = (Q + 31) / 32;
+    const uint32_t nb = want < gridDim.x ? (uint32_t)want : gridDim.x;
+    if (blockIdx.x >= nb) return;  // idle from here on (nb never grows)
+    DIn din{};
+    din.host = a.host;
+    din.relay = a.relay + st;
+    din.err = a.err;
+    din.tag = a.rtag0 + st;
+    Fe ra, rb, rab;
+    block_get_rs(din, ra, rb, rab, nb > 1);
+    const bool two = st > 0 || a.np0 == 2;
+    const uint64_t h4 = 4 * Q;
+    const Fe* X;
+    const Fe* Y;
+    if (st == 0) {
+      X = pp ? a.in[2] : a.in[0];
+      Y = pp ? a.in[3] : a.in[1];
+    } else {
+      const Fe* prev = a.out + dtail_region(a.Q0, st - 1);  // 4 tables of 16 Q
+      X = prev + (uint64_t)(2 * pp) * 16 * Q;
+      Y = prev + (uint64_t)(2 * pp + 1) * 16 * Q;
     }
-    __syncthreads();
-    if (act) {
-      auto q = [&](uint32_t k, uint32_t tab) {
-        Fe r;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) r.v[w] = sc.qs[dq_idx(k, pp, tab, w, jl)];
-        return r;
-      };
-      if (role == 0) {  // alpha = q0 q0, rho = (q0 + q2)^2
-        const Fe q2x = q(2, 0), q2y = q(2, 1);
-        wide_mac<F>(acc0, zx, zy);
-        wide_mac<F>(acc1, fe_add<F>(zx, q2x), fe_add<F>(zy, q2y));
-      } else if (role == 1) {  // delta = q1 q1, e2 = (2q2 - q0)^2 + (2q3 - q1)^2
-        const Fe q0x = q(0, 0), q0y = q(0, 1), q2x = q(2, 0), q2y = q(2, 1), q3x = q(3, 0), q3y = q(3, 1);
-        wide_mac<F>(acc0, zx, zy);
-        wide_mac<F>(acc1, at2<F>(q0x, q2x), at2<F>(q0y, q2y));
-        wide_mac<F>(acc1, at2<F>(zx, q3x), at2<F>(zy, q3y));
-      } else if (role == 2) {  // kappa = q2 q2, W00 = w0 w0
-        const Fe q0x = q(0, 0), q0y = q(0, 1), q1x = q(1, 0), q1y = q(1, 1);
-        wide_mac<F>(acc0, zx, zy);
-        wide_mac<F>(acc1, at2<F>(q0x, q1x), at2<F>(q0y, q1y));
-      } else {  // W11 = w1 w1, Wrho = (w0 + w1)^2
-        const Fe q0x = q(0, 0), q0y = q(0, 1), q1x = q(1, 0), q1y = q(1, 1), q2x = q(2, 0), q2y = q(2, 1);
-        const Fe w1x = at2<F>(q2x, zx), w1y = at2<F>(q2y, zy);
-        wide_mac<F>(acc0, w1x, w1y);
-        wide_mac<F>(acc1, fe_add<F>(at2<F>(q0x, q1x), w1x), fe_add<F>(at2<F>(q0y, q1y), w1y));
+    Fe* Z = a.out + dtail_region(a.Q0, st);
+    Fe* X2 = Z + (uint64_t)(2 * pp) * 4 * Q;
+    Fe* Y2 = Z + (uint64_t)(2 * pp + 1) * 4 * Q;
+    Wide acc0 = wide_zero<F>(), acc1 = wide_zero<F>();
+    for (uint64_t jb = (uint64_t)blockIdx.x * 32; jb < Q; jb += (uint64_t)nb * 32) {
+      const uint64_t j = jb + jl;
+      if (j < Q) {
+        const uint64_t i = j + k * Q;
+        Fe zx, zy;
+        if (two) {
+          zx = fold2<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ld_fe_a(X, i + 2 * h4), ld_fe_a(X, i + 3 * h4), ra, rb, rab);
+          zy = fold2<F>(ld_fe_a(Y, i), ld_fe_a(Y, i + h4), ld_fe_a(Y, i + 2 * h4), ld_fe_a(Y, i + 3 * h4), ra, rb, rab);
+        } else {
+          zx = fold1<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), rb);
+          zy = fold1<F>(ld_fe_a(Y, i), ld_fe_a(Y, i + h4), rb);
+        }
+        st_fe_a(X2, i, zx);
+        st_fe_a(Y2, i, zy);
+        Fe ax, bx, ay, by;
+        grid_points<F>(zx, k, ax, bx);
+        grid_points<F>(zy, k, ay, by);
+        wide_mac<F>(acc0, ax, ay);
+        wide_mac<F>(acc1, bx, by);
       }
     }
-    __syncthreads();  // qs is rewritten by the next iteration
-  }
-  // per-wave column sums: wave w's (acc0, acc1) -> tot[34 w + 17 s + word]
-  uint32_t* rows = sc.rows + role * 64 * 35;
-#pragma unroll
-  for (int w = 0; w < 17; ++w) {
-    rows[lane * 35 + w] = acc0.w[w];
-    rows[lane * 35 + 17 + w] = acc1.w[w];
-  }
-  __syncthreads();
-  if (lane < 34) {
-    uint64_t s0 = 0, s1 = 0;
-#pragma unroll 8
-    for (int r = 0; r < 64; r += 2) {
-      s0 += rows[r * 35 + lane];
-      s1 += rows[(r + 1) * 35 + lane];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores have landed
+    dround_limb_sums(acc0, acc1, sc);
+    RoundSink sk = sink;
+    sk.tag = sink.tag + st;
+    const uint32_t t = threadIdx.x;
+    if (nb > 1) {
+      if (t < (uint32_t)kDLimbs) __hip_atomic_fetch_add(sk.accum + t, sc.tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sc.am_last = prev == nb - 1;
+      }
+      __syncthreads();
+      if (sc.am_last) {
+        if (t < (uint32_t)kDLimbs)
+          sc.tot[t] = __hip_atomic_exchange(sk.accum + t, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        publish_limbs<kDLimbs>(sc, sk);
+      }
+    } else {
+      publish_limbs<kDLimbs>(sc, sk);
     }
-    sc.tot[role * 34 + lane] = s0 + s1;
+    __syncthreads();  // sc is reused next step
   }
-  __syncthreads();
-  grid_finish<kDLimbs>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------
