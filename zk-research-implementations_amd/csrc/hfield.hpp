@@ -1,0 +1,160 @@
+// Host-only field arithmetic on 4 x 64-bit limbs (unsigned __int128 products)
+// for the per-round hand-off: the same values as the 8 x 32-bit ZK_HD
+// templates of field.hpp (Montgomery form, R = 2^256, every result fully
+// reduced), at about a quarter of the instructions. Fe's 8 LE u32 limbs are
+// the same bytes as 4 LE u64 limbs.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include "field.hpp"
+
+namespace zk {
+namespace h64 {
+using u128 = unsigned __int128;
+struct V {
+  uint64_t l[4];
+};
+inline V of(const Fe& x) {
+  V r;
+  memcpy(r.l, x.v, 32);
+  return r;
+}
+inline Fe fe(const V& x) {
+  Fe r;
+  memcpy(r.v, x.l, 32);
+  return r;
+}
+template <class F>
+constexpr uint64_t P(int i) {
+  return (uint64_t)F::P[2 * i] | ((uint64_t)F::P[2 * i + 1] << 32);
+}
+template <class F>
+constexpr uint64_t pinv() {  // -p^-1 mod 2^64 (Newton)
+  uint64_t x = 1;
+  for (int i = 0; i < 7; ++i) x *= 2 - P<F>(0) * x;
+  return (uint64_t)0 - x;
+}
+// x - p if x >= p (x < 2^256 + carry bit `hi`), branch-free
+template <class F>
+inline V sub_p_if_ge(const V& x, uint64_t hi = 0) {
+  V d;
+  unsigned long b = 0;
+  for (int i = 0; i < 4; ++i) d.l[i] = __builtin_subcl(x.l[i], P<F>(i), b, &b);
+  const uint64_t keep = (uint64_t)0 - (uint64_t)(b & (hi ^ 1));  // all ones: x < p, keep x
+  V r;
+  for (int i = 0; i < 4; ++i) r.l[i] = (x.l[i] & keep) | (d.l[i] & ~keep);
+  return r;
+}
+template <class F>
+inline V add(const V& a, const V& b) {  // p < 2^255: no carry out
+  V s;
+  unsigned long c = 0;
+  for (int i = 0; i < 4; ++i) s.l[i] = __builtin_addcl(a.l[i], b.l[i], c, &c);
+  return sub_p_if_ge<F>(s);
+}
+template <class F>
+inline V sub(const V& a, const V& b) {
+  V d;
+  unsigned long bw = 0;
+  for (int i = 0; i < 4; ++i) d.l[i] = __builtin_subcl(a.l[i], b.l[i], bw, &bw);
+  const uint64_t mask = (uint64_t)0 - (uint64_t)bw;
+  unsigned long c = 0;
+  for (int i = 0; i < 4; ++i) d.l[i] = __builtin_addcl(d.l[i], P<F>(i) & mask, c, &c);
+  return d;
+}
+// Montgomery product a b R^-1 mod p (CIOS, 4 x 64)
+template <class F>
+inline V mul(const V& a, const V& b) {
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) {
+    uint64_t C = 0;
+    for (int j = 0; j < 4; ++j) {
+      const u128 s = (u128)a.l[j] * b.l[i] + t[j] + C;
+      t[j] = (uint64_t)s;
+      C = (uint64_t)(s >> 64);
+    }
+    u128 s = (u128)t[4] + C;
+    t[4] = (uint64_t)s;
+    t[5] = (uint64_t)(s >> 64);
+    const uint64_t m = t[0] * pinv<F>();
+    s = (u128)m * P<F>(0) + t[0];
+    C = (uint64_t)(s >> 64);
+    for (int j = 1; j < 4; ++j) {
+      s = (u128)m * P<F>(j) + t[j] + C;
+      t[j - 1] = (uint64_t)s;
+      C = (uint64_t)(s >> 64);
+    }
+    s = (u128)t[4] + C;
+    t[3] = (uint64_t)s;
+    t[4] = t[5] + (uint64_t)(s >> 64);
+  }
+  V r;
+  for (int j = 0; j < 4; ++j) r.l[j] = t[j];
+  return sub_p_if_ge<F>(r, t[4]);
+}
+template <class F>
+inline V reduce(V x) {  // any 256-bit x -> x mod p (2^256 < 6p)
+  for (int k = 0; k < 5; ++k) x = sub_p_if_ge<F>(x);
+  return x;
+}
+template <class F>
+inline V r2() {
+  V r;
+  for (int i = 0; i < 4; ++i) r.l[i] = (uint64_t)F::R2[2 * i] | ((uint64_t)F::R2[2 * i + 1] << 32);
+  return r;
+}
+}  // namespace h64
+
+// Host versions of the field.hpp operations used per round (same results).
+template <class F>
+inline Fe hfe_mul(const Fe& a, const Fe& b) {
+  return h64::fe(h64::mul<F>(h64::of(a), h64::of(b)));
+}
+template <class F>
+inline Fe hfe_add(const Fe& a, const Fe& b) {
+  return h64::fe(h64::add<F>(h64::of(a), h64::of(b)));
+}
+template <class F>
+inline Fe hfe_sub(const Fe& a, const Fe& b) {
+  return h64::fe(h64::sub<F>(h64::of(a), h64::of(b)));
+}
+template <class F>
+inline Fe hfe_from_mont(const Fe& m) {
+  h64::V one = {{1, 0, 0, 0}};
+  return h64::fe(h64::mul<F>(h64::of(m), one));
+}
+template <class F>
+inline Fe hfe_to_mont(const Fe& canon_any) {  // any 256-bit value, reduced mod p first
+  return h64::fe(h64::mul<F>(h64::reduce<F>(h64::of(canon_any)), h64::r2<F>()));
+}
+// limbs_to_fe (field.hpp) on 64-bit limbs
+template <class F>
+inline Fe hlimbs_to_fe(const uint64_t* w, int L, bool product) {
+  // T = sum_i w[i] 2^(32 i): add the even words and the odd words shifted by
+  // 32 into 64-bit limbs with carries
+  uint64_t t[13] = {0};
+  unsigned long c = 0;
+  for (int k = 0; k < 12; ++k) {  // limb k gets w[2k] + (w[2k+1] << 32) + (w[2k-1] >> 32) + carry
+    const uint64_t e = 2 * k < L ? w[2 * k] : 0;
+    const uint64_t o = 2 * k + 1 < L ? w[2 * k + 1] : 0;
+    const uint64_t prev_hi = 2 * k - 1 >= 0 && 2 * k - 1 < L ? (w[2 * k - 1] >> 32) : 0;
+    unsigned long c1 = 0, c2 = 0;
+    uint64_t s = __builtin_addcl(e, o << 32, 0, &c1);
+    s = __builtin_addcl(s, prev_hi, 0, &c2);
+    t[k] = __builtin_addcl(s, c, 0, &c);
+    c += c1 + c2;
+  }
+  h64::V ch[3];
+  for (int k = 0; k < 4; ++k) {
+    ch[0].l[k] = t[k];
+    ch[1].l[k] = t[4 + k];
+    ch[2].l[k] = t[8 + k];
+  }
+  h64::V one = {{1, 0, 0, 0}};
+  if (product)  // REDC(C0) + (C1 mod p) + C2 R   (mul(x, 1) is exact for any x < 2^256)
+    return h64::fe(h64::add<F>(h64::add<F>(h64::mul<F>(ch[0], one), h64::reduce<F>(ch[1])),
+                               h64::mul<F>(h64::reduce<F>(ch[2]), h64::r2<F>())));
+  return h64::fe(h64::add<F>(h64::reduce<F>(ch[0]), h64::mul<F>(h64::reduce<F>(ch[1]), h64::r2<F>())));
+}
+}  // namespace zk

@@ -22,6 +22,7 @@
 #include "field.hpp"
 #include "keccak.hpp"
 #include "kernels.hpp"
+#include "hfield.hpp"
 
 using zk::Fe;
 
@@ -105,7 +106,7 @@ zk_fe out_repr(zk_repr repr, const Fe& m) {  // Montgomery -> host scalar out
 }
 template <class F>
 void canon_bytes(const Fe& m, uint8_t out[32]) {  // into_bigint().to_bytes_le()
-  const Fe c = zk::fe_from_mont<F>(m);
+  const Fe c = zk::hfe_from_mont<F>(m);
   memcpy(out, c.v, 32);
 }
 
@@ -128,9 +129,7 @@ Fe challenge(zk_transcript* t) {
   t->h.update(d, 32);
   Fe x;
   memcpy(x.v, d, 32);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) x = zk::fe_reduce_once<F>(x);  // 2^256 < 6p
-  return zk::fe_to_mont<F>(x);
+  return zk::hfe_to_mont<F>(x);  // LE integer mod p (2^256 < 6p), Montgomery image
 }
 template <class F>
 void absorb(zk_transcript* t, const Fe* m, size_t n) {  // append(fq_vec_to_bytes(v))
@@ -408,7 +407,7 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
     if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
     c->stats.collectives += 1;
   }
-  for (int k = 0; k < K; ++k) out[k] = zk::limbs_to_fe<F>(w + L * k, L, L == 17);
+  for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w + L * k, L, L == 17);
 }
 
 inline void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kSlotU64 * 8); }
@@ -431,8 +430,8 @@ Fe finish_round(zk_transcript* tr, const Fe& e0, const Fe& e1, const Fe& e2, uin
   using namespace zk;
   Fe c[3];
   c[0] = e0;
-  c[2] = fe_mul<F>(fe_add<F>(fe_sub<F>(e0, fe_dbl<F>(e1)), e2), fe_inv2<F>());
-  c[1] = fe_sub<F>(fe_sub<F>(e1, e0), c[2]);
+  c[2] = hfe_mul<F>(hfe_add<F>(hfe_sub<F>(e0, hfe_add<F>(e1, e1)), e2), fe_inv2<F>());
+  c[1] = hfe_sub<F>(hfe_sub<F>(e1, e0), c[2]);
   int m = 3;
   while (m > 0 && fe_is_zero<F>(c[m - 1])) --m;
   absorb<F>(tr, c, (size_t)m);
@@ -441,7 +440,7 @@ Fe finish_round(zk_transcript* tr, const Fe& e0, const Fe& e1, const Fe& e2, uin
   r = challenge<F>(tr);
   out.challenges[k] = r;
   // UnivariatePoly::evaluate(r) (:20-26) via Horner — same field value
-  return fe_add<F>(c[0], fe_mul<F>(r, fe_add<F>(c[1], fe_mul<F>(r, c[2]))));
+  return hfe_add<F>(c[0], hfe_mul<F>(r, hfe_add<F>(c[1], hfe_mul<F>(r, c[2]))));
 }
 
 // Posts the challenge of a finished round to the pinned slot the next
@@ -453,13 +452,20 @@ struct PostR {
   zk_ctx* c;
   uint32_t last = 0;  // highest tag a kernel of this phase waits for (0: none)
   bool done = false;
+  void note() {  // ZK_DEBUG_TAIL: host time from the last result flag to this post
+    if (c->tail_trace)
+      fprintf(stderr, "zk host: flag -> post %.2f us\n",
+              std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->work_t0).count());
+  }
   void post(const Fe& r, uint32_t tag) {
+    note();
     zk::RWait* s = h_rin(c);
     for (int i = 0; i < 8; ++i) __atomic_store_n(&s->r.v[i], r.v[i], __ATOMIC_RELAXED);
     __atomic_store_n(&s->tag, tag, __ATOMIC_RELEASE);
   }
   // the double-round slot: 24 self-tagged words (tag << 32 | limb), any order
   void post2(const Fe& ra, const Fe& rb, const Fe& rab, uint32_t tag) {
+    note();
     zk::RPost* s = h_rpost(c);
     const uint64_t t = (uint64_t)tag << 32;
     for (int i = 0; i < 8; ++i) {
@@ -623,6 +629,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       rtags[si] = c->rtag + 1;
       c->rtag += st.nd;
       a.rtag0 = rtags[si];
+      if (c->tail_trace) a.trace = c->tail_trace;
       const uint32_t grid = (uint32_t)std::min<uint64_t>(
           {(Q0 + 31) / 32, (uint64_t)std::min<uint32_t>(c->dtail_blocks, 64u), (uint64_t)c->num_cus});
       double bytes = 0, muls = 0;
@@ -712,7 +719,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const GStep& nx = steps[si + 1];
     if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
       if (nx.np == 2)
-        post.post2(ra, rb, zk::fe_mul<F>(ra, rb), rtags[si + 1]);
+        post.post2(ra, rb, zk::hfe_mul<F>(ra, rb), rtags[si + 1]);
       else
         post.post2(zk::fe_zero<F>(), rb, zk::fe_zero<F>(), rtags[si + 1]);
     } else {
@@ -730,19 +737,19 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       collect_sums<F, zk::kDCats>(c, sinks[i0], across_ranks, 17, d);
       // categories: 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21, 7 V12 (kernels.hpp)
       // round i: e0 = V00 + V01, e2 = V20 + V21
-      const Fe e0 = zk::fe_add<F>(d[0], d[2]);
-      one_round(i0, e0, zk::fe_sub<F>(claim, e0), zk::fe_add<F>(d[5], d[6]));
+      const Fe e0 = zk::hfe_add<F>(d[0], d[2]);
+      one_round(i0, e0, zk::hfe_sub<F>(claim, e0), zk::hfe_add<F>(d[5], d[6]));
       // round i + 1 at r = r_i: e0' through (V00, V10, V20), e2' through (V02, V12, V22) at r = 0, 1, 2
-      const Fe one = zk::fe_one<F>(), two = zk::fe_add<F>(one, one), h = zk::fe_inv2<F>();
-      const Fe rm1 = zk::fe_sub<F>(r, one), rm2 = zk::fe_sub<F>(r, two);
-      const Fe L0 = zk::fe_mul<F>(zk::fe_mul<F>(rm1, rm2), h);                 // (r-1)(r-2)/2
-      const Fe L1 = zk::fe_sub<F>(zk::fe_zero<F>(), zk::fe_mul<F>(r, rm2));     // -r(r-2)
-      const Fe L2 = zk::fe_mul<F>(zk::fe_mul<F>(r, rm1), h);                   // r(r-1)/2
+      const Fe one = zk::fe_one<F>(), two = zk::hfe_add<F>(one, one), h = zk::fe_inv2<F>();
+      const Fe rm1 = zk::hfe_sub<F>(r, one), rm2 = zk::hfe_sub<F>(r, two);
+      const Fe L0 = zk::hfe_mul<F>(zk::hfe_mul<F>(rm1, rm2), h);                 // (r-1)(r-2)/2
+      const Fe L1 = zk::hfe_sub<F>(zk::fe_zero<F>(), zk::hfe_mul<F>(r, rm2));     // -r(r-2)
+      const Fe L2 = zk::hfe_mul<F>(zk::hfe_mul<F>(r, rm1), h);                   // r(r-1)/2
       auto lag = [&](const Fe& v0, const Fe& v1, const Fe& v2) {
-        return zk::fe_add<F>(zk::fe_add<F>(zk::fe_mul<F>(L0, v0), zk::fe_mul<F>(L1, v1)), zk::fe_mul<F>(L2, v2));
+        return zk::hfe_add<F>(zk::hfe_add<F>(zk::hfe_mul<F>(L0, v0), zk::hfe_mul<F>(L1, v1)), zk::hfe_mul<F>(L2, v2));
       };
       const Fe f0 = lag(d[0], d[4], d[5]), f2 = lag(d[3], d[7], d[1]);
-      one_round(i0 + 1, f0, zk::fe_sub<F>(claim, f0), f2);
+      one_round(i0 + 1, f0, zk::hfe_sub<F>(claim, f0), f2);
   };
   for (size_t si = 0; si < ns; ++si) {
     const GStep& st = steps[si];
@@ -755,13 +762,13 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     } else if (st.kind == GS_SINGLE) {
       Fe s2[2];
       collect_sums<F, 2>(c, sinks[st.i], across_ranks, 17, s2);
-      one_round(st.i, s2[0], zk::fe_sub<F>(claim, s2[0]), s2[1]);
+      one_round(st.i, s2[0], zk::hfe_sub<F>(claim, s2[0]), s2[1]);
       pend = 1;
     } else if (st.kind == GS_TAIL) {
       for (uint32_t i = st.i; i < nv; ++i) {
         Fe s2[2];
         collect_sums<F, 2>(c, sinks[i], across_ranks, 17, s2);
-        one_round(i, s2[0], zk::fe_sub<F>(claim, s2[0]), s2[1]);
+        one_round(i, s2[0], zk::hfe_sub<F>(claim, s2[0]), s2[1]);
         if (pre && i + 1 < nv) post.post(r, rtags[si] + (i + 1 - st.i));
       }
       pend = 1;
@@ -771,7 +778,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     } else {  // GS_DTAIL
       for (uint32_t d = 0; d < st.nd; ++d) {
         two_rounds(st.i + 2 * d);
-        if (d + 1 < st.nd) post.post2(ra, rb, zk::fe_mul<F>(ra, rb), rtags[si] + d + 1);
+        if (d + 1 < st.nd) post.post2(ra, rb, zk::hfe_mul<F>(ra, rb), rtags[si] + d + 1);
       }
       pend = 2;
     }
@@ -786,6 +793,16 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       fprintf(stderr, "zk tail round %2u: wait r %6.2f us, fold+eval %6.2f, fan-in %6.2f, publish %6.2f, hand-off to next r %6.2f\n",
               m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
               (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, m + 1 < nr ? (T[m * 8 + 9] - T[m * 8 + 4]) * 0.01 : 0.0);
+  }
+  if (c->tail_trace && !steps.empty() && steps.back().kind == GS_DTAIL) {  // ZK_DEBUG_TAIL
+    HIPCK(hipStreamSynchronize(c->stream));
+    const uint64_t* T = c->tail_trace;
+    const uint32_t nd = steps.back().nd;
+    for (uint32_t m = 0; m < nd; ++m)
+      fprintf(stderr, "zk dtail step %u: wait r %6.2f us, fold+eval %6.2f, limb sums %6.2f, fan-in %6.2f, publish %6.2f, hand-off to next r %6.2f\n",
+              m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
+              (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, (T[m * 8 + 5] - T[m * 8 + 4]) * 0.01,
+              m + 1 < nd ? (T[m * 8 + 9] - T[m * 8 + 5]) * 0.01 : 0.0);
   }
 }
 

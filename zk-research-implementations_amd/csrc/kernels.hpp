@@ -884,6 +884,7 @@ struct DTailArgs {
   const RPost* host;  // pinned challenge words
   RPost* relay;       // nsteps fresh relay slots
   uint32_t* err;      // pinned error word
+  uint64_t* trace;    // debug (ZK_DEBUG_TAIL): per step 8 s_memrealtime stamps, or null
 };
 __host__ __device__ __forceinline__ uint64_t dtail_region(uint64_t Q0, uint32_t s) {
   uint64_t o = 0;
@@ -907,7 +908,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     din.err = a.err;
     din.tag = a.rtag0 + st;
     Fe ra, rb, rab;
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     block_get_rs(din, ra, rb, rab, nb > 1);
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 1] = __builtin_amdgcn_s_memrealtime();
     const bool two = st > 0 || a.np0 == 2;
     const uint64_t h4 = 4 * Q;
     const Fe* X;
@@ -946,7 +949,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores have landed
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 2] = __builtin_amdgcn_s_memrealtime();
     dround_limb_sums(acc0, acc1, sc);
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 3] = __builtin_amdgcn_s_memrealtime();
     RoundSink sk = sink;
     sk.tag = sink.tag + st;
     const uint32_t t = threadIdx.x;
@@ -963,10 +968,14 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
         if (t < (uint32_t)kDLimbs)
           sc.tot[t] = __hip_atomic_exchange(sk.accum + t, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.trace && t == 0) a.trace[st * 8 + 4] = __builtin_amdgcn_s_memrealtime();
         publish_limbs<kDLimbs>(sc, sk);
+        if (a.trace && t == 0) a.trace[st * 8 + 5] = __builtin_amdgcn_s_memrealtime();
       }
     } else {
+      if (a.trace && t == 0) a.trace[st * 8 + 4] = __builtin_amdgcn_s_memrealtime();
       publish_limbs<kDLimbs>(sc, sk);
+      if (a.trace && t == 0) a.trace[st * 8 + 5] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();  // sc is reused next step
   }
