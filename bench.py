@@ -338,7 +338,7 @@ def main() -> None:
             # during the LAST timed step only: their marker packets cost the GPU
             # ~5 us per round, so timing every step would inflate ms_per_step
             st0 = ctx.stats()
-            ctx.set_timing_kinds([] if args.no_events else ["gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail"])
+            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail"])
         step()
     torch.cuda.synchronize()
     barrier()
@@ -355,15 +355,31 @@ def main() -> None:
     value = ops / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     k = st["kernels"]
-    # the dominant kernel (k_gkr_round: the large rounds) and the small rounds'
-    # k_gkr_round_lanes, over the event-timed (last) step
+    # per kernel kind over the event-timed (last) step; the dominant kernel is
+    # k_gkr_round (round 1: the longest launch of the proof)
     def kind(name):
         d = {f: k[name][f] - st0["kernels"][name][f] for f in ("launches", "alg_bytes")}
         d["ms"] = k[name]["ms"]
         return d
 
-    rnd, lanes, tail = kind("gkr_round"), kind("gkr_round_lanes"), kind("gkr_tail")
-    small = {f: lanes[f] + tail[f] for f in ("launches", "alg_bytes", "ms")}
+    rnd = kind("gkr_round")
+    round_kinds = {
+        "gkr_round0": "k_gkr_round0 (round 0: e0, e1, e2 over the input tables)",
+        "gkr_round": "k_gkr_round (round 1: fold by r0 + round sums)",
+        "gkr_round_lanes": "k_gkr_round_lanes (single small rounds, 8 lanes per pair)",
+        "gkr_dround": "k_gkr_dround (two rounds per launch: pending folds + round m sums + round m+1 quadratics)",
+        "gkr_dtail": "k_gkr_dtail (the small double steps in one persistent kernel; host hand-offs included)",
+        "gkr_tail": "k_gkr_tail (ZK_DROUND=0: small single rounds in one persistent kernel)",
+    }
+    per_kind = {}
+    for name, desc in round_kinds.items():
+        d = kind(name)
+        if d["launches"]:
+            per_kind[name] = {"kernel": desc, "launches": d["launches"], "ms": d["ms"],
+                              "alg_GB": d["alg_bytes"] / 1e9,
+                              "achieved_GBs": d["alg_bytes"] / (d["ms"] / 1e3) / 1e9 if d["ms"] else None}
+    all_b = sum(kind(nm)["alg_bytes"] for nm in per_kind)
+    all_ms = sum(kind(nm)["ms"] for nm in per_kind)
     achieved = rnd["alg_bytes"] / (rnd["ms"] / 1e3) / 1e9 if rnd["ms"] else 0.0
     kernel_ms = sum(v["ms"] for v in k.values())  # the timed (last) step
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
@@ -400,7 +416,7 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gkr_round (fused fold + round evaluation; rounds with > 2^15 pairs)",
+                "kernel": "k_gkr_round (round 1: fused fold by r0 + round evaluation; the longest launch)",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -411,16 +427,8 @@ def main() -> None:
                 "avg_launch_us": rnd["ms"] * 1e3 / max(1, rnd["launches"]),
                 "alg_bytes_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]),
                 "alg_GB_per_launch": rnd["alg_bytes"] / max(1, rnd["launches"]) / 1e9,
-                "small_rounds": {
-                    "kernel": "k_gkr_tail (rounds with <= 2^15 pairs in one persistent kernel, host hand-off "
-                    "between rounds included; latency-bound)" if tail["launches"] else
-                    "k_gkr_round_lanes (rounds with <= 2^15 pairs, latency-bound)",
-                    "launches": small["launches"],
-                    "ms": small["ms"],
-                    "achieved_GBs": small["alg_bytes"] / (small["ms"] / 1e3) / 1e9 if small["ms"] else None,
-                },
-                "all_rounds_GBs": (rnd["alg_bytes"] + small["alg_bytes"]) / ((rnd["ms"] + small["ms"]) / 1e3) / 1e9
-                if rnd["ms"] + small["ms"] else None,
+                "round_kernels": per_kind,
+                "all_rounds_GBs": all_b / (all_ms / 1e3) / 1e9 if all_ms else None,
             },
             "breakdown_per_step": {
                 "wall_ms": ms_per_step,

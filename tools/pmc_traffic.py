@@ -1,12 +1,17 @@
-"""HBM traffic of the dominant kernel from rocprofv3 PMC passes.
+"""HBM traffic of the round kernels from rocprofv3 PMC passes.
 
 Reads gpurun_out/prof_<tag>_fetch and _write (FETCH_SIZE / WRITE_SIZE, KiB per
-dispatch), takes the k_gkr_round dispatches of the LAST proof in the run, and
-reports per-launch traffic = 2 * FETCH_SIZE + WRITE_SIZE bytes (the x2 is the
-gfx950 correction for wide coalesced streaming reads, MI355X_MICROARCH.md
-"HBM"), beside the algorithmic bytes (768 B per output pair).
+dispatch), takes the dispatches of the LAST proof in the run (from its
+k_gkr_round0), and reports per dispatch traffic = 2 * FETCH_SIZE + WRITE_SIZE
+bytes (the x2 is the gfx950 correction for wide coalesced streaming reads,
+MI355X_MICROARCH.md "HBM") beside the algorithmic bytes of the step schedule
+(host.hpp gkr_phase): round 0 256 B per pair, a single round 768 B per output
+pair, a double step 1536 B (one pending challenge) or 2560 B (two) per quad,
+the persistent tail the sum of its double steps.
 Writes profiles/<tag>_traffic.json and copies the kernel-stats CSV.
-usage: python tools/pmc_traffic.py <tag> <nvars>
+usage: python tools/pmc_traffic.py <tag> <nvars> [dtail_max_quads]
+(tools/profile_bench.sh launches steps one at a time, ZK_PRELAUNCH=0: no persistent
+tail, so dtail_max_quads defaults to 0)
 """
 import csv
 import json
@@ -14,55 +19,79 @@ import os
 import shutil
 import sys
 
-KERNEL = "zk::k_gkr_round"
-
 
 def dispatches(path, counter):
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     out = {}
     for r in rows:
-        out[int(r["Dispatch_Id"])] = (r["Kernel_Name"], int(r["Grid_Size"]), float(r["Counter_Value"]))
+        out[int(r["Dispatch_Id"])] = (r["Kernel_Name"].split("(")[0].replace("void ", ""), float(r["Counter_Value"]))
     return [out[k] for k in sorted(out)]
+
+
+def schedule(n, dtail_max_quads=4096):
+    """(symbol prefix, algorithmic bytes) per dispatch of one proof (pre-enqueued, one GPU)."""
+    st = [("zk::k_gkr_round0", 256.0 * (1 << (n - 1)))]
+    if n >= 2:
+        st.append(("zk::k_gkr_round", 768.0 * (1 << (n - 2))))
+    i = 2
+    if n >= 3 and (n - 2) % 2 == 1:
+        st.append(("zk::k_gkr_round", 768.0 * (1 << (n - 3))))
+        i = 3
+    doubles = []
+    np_ = 1
+    while i + 1 < n:
+        q = (1 << (n - i)) // 4
+        doubles.append((q, np_))
+        np_, i = 2, i + 2
+    d0 = next((k for k, (q, _) in enumerate(doubles) if q <= dtail_max_quads), len(doubles))
+    if len(doubles) - d0 < 2:
+        d0 = len(doubles)
+    for q, p in doubles[:d0]:
+        st.append((f"zk::k_gkr_dround<zk::Bn254Fr, {p}>", (1536.0 if p == 1 else 2560.0) * q))
+    if d0 < len(doubles):
+        st.append(("zk::k_gkr_dtail", sum((1536.0 if p == 1 else 2560.0) * q for q, p in doubles[d0:])))
+    return st
 
 
 def main():
     tag, nvars = sys.argv[1], int(sys.argv[2])
+    dmax = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     fetch = dispatches(f"{root}/gpurun_out/prof_{tag}_fetch/run_counter_collection.csv", "FETCH_SIZE")
     write = dispatches(f"{root}/gpurun_out/prof_{tag}_write/run_counter_collection.csv", "WRITE_SIZE")
-    rounds = nvars - 1  # k_gkr_round(+_lanes) launches per proof
-    f = [x for x in fetch if KERNEL in x[0]][-rounds:]
-    w = [x for x in write if KERNEL in x[0]][-rounds:]
-    assert len(f) == len(w) == rounds
-    per_round = []
-    for k, ((name, _, fe), (_, _, wr)) in enumerate(zip(f, w), start=1):
-        pairs = 1 << (nvars - 1 - k)
-        per_round.append({"round": k, "kernel": name.split("(")[0], "fetch_bytes": 2 * fe * 1024,
-                          "write_bytes": wr * 1024, "alg_bytes": 768.0 * pairs})
-    # the dominant kernel is the symbol k_gkr_round (large rounds); the small
-    # rounds' k_gkr_round_lanes is summarised beside it
-    def summary(sym):
-        rs = [r for r in per_round if r["kernel"].endswith(sym)]
+    sched = schedule(nvars, dmax)
+
+    def last_proof(ds):
+        start = max(k for k, d in enumerate(ds) if "k_gkr_round0" in d[0])
+        return [d for d in ds[start:] if "k_gkr_" in d[0]][: len(sched)]
+
+    f, w = last_proof(fetch), last_proof(write)
+    assert len(f) == len(w) == len(sched), (len(f), len(w), len(sched))
+    steps = []
+    for (sym, alg), (name, fe), (_, wr) in zip(sched, f, w):
+        assert name.startswith(sym.split("<")[0]), (name, sym)
+        steps.append({"kernel": name, "fetch_bytes": 2 * fe * 1024, "write_bytes": wr * 1024, "alg_bytes": alg})
+
+    def summary(pred):
+        rs = [r for r in steps if pred(r["kernel"])]
         t = sum(r["fetch_bytes"] + r["write_bytes"] for r in rs)
         a = sum(r["alg_bytes"] for r in rs)
-        return rs, t, a
+        return {"launches": len(rs), "traffic_bytes_per_launch": t / max(1, len(rs)),
+                "alg_bytes_per_launch": a / max(1, len(rs)), "traffic_over_alg": t / a if a else None}
 
-    big, tot_traffic, tot_alg = summary("k_gkr_round<zk::Bn254Fr>")
-    lanes, lt, la = summary("k_gkr_round_lanes<zk::Bn254Fr>")
-    res = {"kernel": "k_gkr_round", "nvars": nvars, "launches": len(big),
-           "traffic_bytes_per_launch": tot_traffic / len(big), "alg_bytes_per_launch": tot_alg / len(big),
-           "traffic_over_alg": tot_traffic / tot_alg,
-           "lanes": {"kernel": "k_gkr_round_lanes", "launches": len(lanes),
-                     "traffic_bytes_per_launch": lt / max(1, len(lanes)), "alg_bytes_per_launch": la / max(1, len(lanes)),
-                     "traffic_over_alg": lt / la if la else None},
+    big = summary(lambda k: k.startswith("zk::k_gkr_round<"))
+    res = {"kernel": "k_gkr_round", "nvars": nvars, **big,
+           "others": {"k_gkr_round0": summary(lambda k: "k_gkr_round0" in k),
+                      "k_gkr_dround": summary(lambda k: "k_gkr_dround" in k),
+                      "k_gkr_dtail": summary(lambda k: "k_gkr_dtail" in k)},
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                      "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 half-count correction)",
-           "per_round": per_round}
+           "per_step": steps}
     os.makedirs(f"{root}/profiles", exist_ok=True)
     with open(f"{root}/profiles/{tag}_traffic.json", "w") as fh:
         json.dump(res, fh, indent=1)
     shutil.copy(f"{root}/gpurun_out/prof_{tag}/run_kernel_stats.csv", f"{root}/profiles/{tag}_kernel_stats.csv")
-    print(json.dumps({k: v for k, v in res.items() if k != "per_round"}, indent=1))
+    print(json.dumps({k: v for k, v in res.items() if k != "per_step"}, indent=1))
 
 
 if __name__ == "__main__":
