@@ -203,7 +203,7 @@ struct zk_ctx {
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
-  uint64_t dtail_max_quads = 1u << 12;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
+  uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
   bool tail = true;         // (ZK_DROUND=0 only) pre-enqueued small rounds in one persistent kernel (ZK_TAIL=0: one launch each)
   uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
@@ -631,7 +631,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       a.rtag0 = rtags[si];
       if (c->tail_trace) a.trace = c->tail_trace;
       const uint32_t grid = (uint32_t)std::min<uint64_t>(
-          {(Q0 + 31) / 32, (uint64_t)std::min<uint32_t>(c->dtail_blocks, 64u), (uint64_t)c->num_cus});
+          {(Q0 + zk::kDQuads - 1) / zk::kDQuads, (uint64_t)std::min<uint32_t>(c->dtail_blocks, 64u), (uint64_t)c->num_cus});
       double bytes = 0, muls = 0;
       for (uint32_t d = 0; d < st.nd; ++d) {
         const bool two = d > 0 || st.np == 2;
@@ -662,7 +662,8 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       } else {
         din.rb = rb;
       }
-      const uint32_t grid = grid_for(c, 8 * Q, zk::k_gkr_dround<F, 2>);
+      const uint32_t grid = st.np == 2 ? grid_for(c, zk::kDQuads * Q, zk::k_gkr_dround<F, 2>)
+                                       : grid_for(c, zk::kDQuads * Q, zk::k_gkr_dround<F, 1>);
       const double bytes = (st.np == 2 ? 2560.0 : 1536.0) * Q, muls = (st.np == 2 ? 40.0 : 24.0) * Q;
       if (st.np == 2)
         launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dround<F, 2>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],

@@ -693,13 +693,15 @@ __global__ __launch_bounds__(kBlock) void k_gkr_tail(TailArgs a, RoundSink sink)
 //               X(2) = V(r,2), so e0'(r) and e2'(r) are quadratics in r given
 //               by their values at r = 0, 1, 2: V(.,0)^2 and V(.,2)^2.
 // ("V^2" = the A-side value times the S-side value, plus M times P.) That is
-// the 3x3 grid without its centre: 8 product sums, two per lane. Lane k of
-// the 4 lanes of a quad holds corner k and forms, by quad_perm DPP moves
-// (no LDS, no barrier), the extended point it multiplies:
+// the 3x3 grid without its centre: 8 product sums. A quad of one product
+// (A*S or M*P) is a unit of 8 lanes, 4 tab + k: lane k of table tab computes
+// corner k (one fold per lane) and forms, by quad_perm DPP moves (no LDS, no
+// barrier), its two grid points:
 //   k = 0 (0,0): V(0,0), V(2,2)     k = 1 (0,1): V(0,1), V(0,2)
 //   k = 2 (1,0): V(1,0), V(2,0)     k = 3 (1,1): V(2,1), V(1,2)
-// Category c = 2k + slot: 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21,
-// 7 V12 (limb sums of values in [0, p): exact). The host finishes round m,
+// then trades one point with its partner in the other table (lane ^ 4) and
+// multiplies slot tab + 1. Category c = 2k + slot: 0 V00, 1 V22, 2 V01,
+// 3 V02, 4 V10, 5 V20, 6 V21, 7 V12 (limb sums of values in [0, p): exact). The host finishes round m,
 // draws r_m, interpolates round m+1's values at r_m, draws r_{m+1} and posts
 // (r_m, r_{m+1}, r_m r_{m+1}): one hand-off and one kernel per two rounds.
 //
@@ -758,8 +760,9 @@ __device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& 
 
 constexpr int kDCats = 8;             // product-sum categories of a double round
 constexpr int kDLimbs = kDCats * 17;  // 136 limb sums
+constexpr uint32_t kDQuads = 16;      // quads per block iteration (8 lanes each: 2 tables x 4 corners, 2 products)
 struct DScratch {
-  uint32_t rows[kBlock * 35];  // limb-sum transpose: 2 x 17 words per thread (odd stride)
+  uint32_t rows[kBlock * 17];  // limb-sum transpose: 17 words per thread (odd stride)
   uint64_t tot[kSlotU64];
   uint64_t pp[kBlock];
   uint32_t am_last;
@@ -770,6 +773,13 @@ __device__ __forceinline__ Fe dpp_fe(const Fe& x) {
   Fe r;
 #pragma unroll
   for (int w = 0; w < 8; ++w) r.v[w] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[w], CTRL, 0xF, 0xF, false);
+  return r;
+}
+// lane i reads lane i ^ 4 (ds_swizzle bit mode: and 0x1F, xor 4; no LDS memory)
+__device__ __forceinline__ Fe xor4_fe(const Fe& x) {
+  Fe r;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) r.v[w] = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x.v[w], 0x101F);
   return r;
 }
 __device__ __forceinline__ Fe sel_fe(bool c, const Fe& a, const Fe& b) {
@@ -788,24 +798,33 @@ __device__ __forceinline__ void grid_points(const Fe& q, uint32_t k, Fe& s1, Fe&
   s1 = sel_fe(k == 3, e1, q);
   s2 = sel_fe(k == 0 || k == 3, e2, e1);
 }
-
-// limb sums: category c = 2k + s over the 64 threads of the block with lane & 3 == k
-// -> sc.tot[17 c + word] (valid after the call)
-__device__ __forceinline__ void dround_limb_sums(const Wide& acc0, const Wide& acc1, DScratch& sc) {
+// One quad-product unit = 8 lanes: lane u = 4 tab + k holds corner k of table
+// tab (A or M for tab 0, S or P for tab 1). After grid_points each lane owns
+// the product of slot tab + 1: it sends the other slot's point to its partner
+// lane (u ^ 4) and multiplies its own point by the partner's. Category of a
+// lane: c = 2k + tab.
+template <class F>
+__device__ __forceinline__ void unit_product(const Fe& z, uint32_t k, uint32_t tab, Wide& acc) {
+  Fe s1, s2;
+  grid_points<F>(z, k, s1, s2);
+  const Fe mine = tab ? s2 : s1;
+  const Fe other = xor4_fe(tab ? s1 : s2);
+  wide_mac<F>(acc, mine, other);
+}
+// limb sums of one accumulator per thread: category c = 2k + tab over the
+// threads with (lane & 7) == 4 tab + k -> sc.tot[17 c + word] (valid after the call)
+__device__ __forceinline__ void dround_limb_sums(const Wide& acc, DScratch& sc) {
 #pragma unroll
-  for (int w = 0; w < 17; ++w) {
-    sc.rows[threadIdx.x * 35 + w] = acc0.w[w];
-    sc.rows[threadIdx.x * 35 + 17 + w] = acc1.w[w];
-  }
+  for (int w = 0; w < 17; ++w) sc.rows[threadIdx.x * 17 + w] = acc.w[w];
   __syncthreads();
   const uint32_t t = threadIdx.x;
   if (t < (uint32_t)kDLimbs) {
-    const uint32_t c = t / 17, w = t % 17, kk = c >> 1, off = (c & 1) * 17 + w;
+    const uint32_t c = t / 17, w = t % 17, u = 4 * (c & 1) + (c >> 1);
     uint64_t s0 = 0, s1 = 0;
 #pragma unroll 8
-    for (uint32_t m = 0; m < 64; m += 2) {
-      s0 += sc.rows[(4 * m + kk) * 35 + off];
-      s1 += sc.rows[(4 * m + 4 + kk) * 35 + off];
+    for (uint32_t m = 0; m < kBlock / 8; m += 2) {
+      s0 += sc.rows[(8 * m + u) * 17 + w];
+      s1 += sc.rows[(8 * m + 8 + u) * 17 + w];
     }
     sc.tot[t] = s0 + s1;
   }
@@ -822,49 +841,39 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
   Fe ra, rb, rab;
   block_get_rs(din, ra, rb, rab, gridDim.x > 1);
   __shared__ DScratch sc;
-  // wave w: product w & 1 (A*S or M*P), quads (w >> 1) * 16 + [0, 16) of each 32
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3;
-  const uint32_t pp = wv & 1, jl = (wv >> 1) * 16 + (lane >> 2);
-  const Fe* __restrict__ X = pp ? M : A;
-  const Fe* __restrict__ Y = pp ? P : S;
-  Fe* __restrict__ X2 = pp ? M2 : A2;
-  Fe* __restrict__ Y2 = pp ? P2 : S2;
+  // wave w: product w & 1 (A*S or M*P), quads (w >> 1) * 8 + [0, 8) of each 16; lane = 8 unit + 4 tab + k
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1;
+  const uint32_t pp = wv & 1, jl = (wv >> 1) * 8 + (lane >> 3);
+  const Fe* __restrict__ X = pp ? (tab ? P : M) : (tab ? S : A);
+  Fe* __restrict__ X2 = pp ? (tab ? P2 : M2) : (tab ? S2 : A2);
   const uint64_t h4 = 4 * Q;
-  Wide acc0 = wide_zero<F>(), acc1 = wide_zero<F>();
-  for (uint64_t jb = (uint64_t)blockIdx.x * 32; jb < Q; jb += (uint64_t)gridDim.x * 32) {
+  Wide acc = wide_zero<F>();
+  for (uint64_t jb = (uint64_t)blockIdx.x * kDQuads; jb < Q; jb += (uint64_t)gridDim.x * kDQuads) {
     const uint64_t j = jb + jl;
-    if (j < Q) {  // uniform over the 4 lanes of a quad
+    if (j < Q) {  // uniform over the 8 lanes of a unit
       const uint64_t i = j + k * Q;
-      Fe zx, zy;
+      Fe z;
       if (NP == 2) {
         const Fe x00 = ld_fe(X, i), x01 = ld_fe(X, i + h4), x10 = ld_fe(X, i + 2 * h4), x11 = ld_fe(X, i + 3 * h4);
-        const Fe y00 = ld_fe(Y, i), y01 = ld_fe(Y, i + h4), y10 = ld_fe(Y, i + 2 * h4), y11 = ld_fe(Y, i + 3 * h4);
         __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
-        zx = fold2<F>(x00, x01, x10, x11, ra, rb, rab);
-        zy = fold2<F>(y00, y01, y10, y11, ra, rb, rab);
+        z = fold2<F>(x00, x01, x10, x11, ra, rb, rab);
       } else {
-        const Fe x0 = ld_fe(X, i), x1 = ld_fe(X, i + h4), y0 = ld_fe(Y, i), y1 = ld_fe(Y, i + h4);
+        const Fe x0 = ld_fe(X, i), x1 = ld_fe(X, i + h4);
         __builtin_amdgcn_sched_barrier(0);
-        zx = fold1<F>(x0, x1, rb);
-        zy = fold1<F>(y0, y1, rb);
+        z = fold1<F>(x0, x1, rb);
       }
-      st_fold(X2, i, zx);
-      st_fold(Y2, i, zy);
-      Fe ax, bx, ay, by;
-      grid_points<F>(zx, k, ax, bx);
-      grid_points<F>(zy, k, ay, by);
-      wide_mac<F>(acc0, ax, ay);
-      wide_mac<F>(acc1, bx, by);
+      st_fold(X2, i, z);
+      unit_product<F>(z, k, tab, acc);
     }
   }
-  dround_limb_sums(acc0, acc1, sc);
+  dround_limb_sums(acc, sc);
   grid_finish<kDLimbs>(sc, sink);
 }
 
 // ---------------------------------------------------------------------------
 // The small double rounds of a proof in ONE persistent kernel: step s is the
 // k_gkr_dround step over Q0 >> 2s quads (two pending challenges, the first
-// step np0), run by min(gridDim, Q/32) blocks. The instruction cache stays
+// step np0), run by min(gridDim, Q/16) blocks. The instruction cache stays
 // warm and no launch sits between steps; per step block 0 waits for the
 // host's three challenges (tag rtag0 + s) and relays them through a fresh
 // slot, the active blocks fold and evaluate, their 136 limb sums meet in the
@@ -895,11 +904,12 @@ __host__ __device__ __forceinline__ uint64_t dtail_region(uint64_t Q0, uint32_t 
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sink) {
   __shared__ DScratch sc;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3;
-  const uint32_t pp = wv & 1, jl = (wv >> 1) * 16 + (lane >> 2);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1;
+  const uint32_t pp = wv & 1, jl = (wv >> 1) * 8 + (lane >> 3);
+  const uint32_t tb = 2 * pp + tab;  // table A, S, M, P
   for (uint32_t st = 0; st < a.nsteps; ++st) {
     const uint64_t Q = a.Q0 >> (2 * st);
-    const uint64_t want = (Q + 31) / 32;
+    const uint64_t want = (Q + kDQuads - 1) / kDQuads;
     const uint32_t nb = want < gridDim.x ? (uint32_t)want : gridDim.x;
     if (blockIdx.x >= nb) return;  // idle from here on (nb never grows)
     DIn din{};
@@ -914,43 +924,27 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     const bool two = st > 0 || a.np0 == 2;
     const uint64_t h4 = 4 * Q;
     const Fe* X;
-    const Fe* Y;
     if (st == 0) {
-      X = pp ? a.in[2] : a.in[0];
-      Y = pp ? a.in[3] : a.in[1];
+      X = a.in[tb];
     } else {
       const Fe* prev = a.out + dtail_region(a.Q0, st - 1);  // 4 tables of 16 Q
-      X = prev + (uint64_t)(2 * pp) * 16 * Q;
-      Y = prev + (uint64_t)(2 * pp + 1) * 16 * Q;
+      X = prev + (uint64_t)tb * 16 * Q;
     }
-    Fe* Z = a.out + dtail_region(a.Q0, st);
-    Fe* X2 = Z + (uint64_t)(2 * pp) * 4 * Q;
-    Fe* Y2 = Z + (uint64_t)(2 * pp + 1) * 4 * Q;
-    Wide acc0 = wide_zero<F>(), acc1 = wide_zero<F>();
-    for (uint64_t jb = (uint64_t)blockIdx.x * 32; jb < Q; jb += (uint64_t)nb * 32) {
+    Fe* X2 = a.out + dtail_region(a.Q0, st) + (uint64_t)tb * 4 * Q;
+    Wide acc = wide_zero<F>();
+    for (uint64_t jb = (uint64_t)blockIdx.x * kDQuads; jb < Q; jb += (uint64_t)nb * kDQuads) {
       const uint64_t j = jb + jl;
       if (j < Q) {
         const uint64_t i = j + k * Q;
-        Fe zx, zy;
-        if (two) {
-          zx = fold2<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ld_fe_a(X, i + 2 * h4), ld_fe_a(X, i + 3 * h4), ra, rb, rab);
-          zy = fold2<F>(ld_fe_a(Y, i), ld_fe_a(Y, i + h4), ld_fe_a(Y, i + 2 * h4), ld_fe_a(Y, i + 3 * h4), ra, rb, rab);
-        } else {
-          zx = fold1<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), rb);
-          zy = fold1<F>(ld_fe_a(Y, i), ld_fe_a(Y, i + h4), rb);
-        }
-        st_fe_a(X2, i, zx);
-        st_fe_a(Y2, i, zy);
-        Fe ax, bx, ay, by;
-        grid_points<F>(zx, k, ax, bx);
-        grid_points<F>(zy, k, ay, by);
-        wide_mac<F>(acc0, ax, ay);
-        wide_mac<F>(acc1, bx, by);
+        const Fe z = two ? fold2<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ld_fe_a(X, i + 2 * h4), ld_fe_a(X, i + 3 * h4), ra, rb, rab)
+                         : fold1<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), rb);
+        st_fe_a(X2, i, z);
+        unit_product<F>(z, k, tab, acc);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores have landed
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-    dround_limb_sums(acc0, acc1, sc);
+    dround_limb_sums(acc, sc);
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 3] = __builtin_amdgcn_s_memrealtime();
     RoundSink sk = sink;
     sk.tag = sink.tag + st;
