@@ -347,6 +347,7 @@ inline void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
 
 inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   zk::RoundSink s;
+  s.trace = c->tail_trace ? c->tail_trace + 512 : nullptr;  // ZK_DEBUG_TAIL: per-step stamps
   s.partials = reinterpret_cast<uint64_t*>(c->partials.p);
   s.counter = d_counter(c);
   s.accum = d_accum(c);
@@ -786,6 +787,20 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     hand_on(si);
   }
   post.done = true;
+  if (c->tail_trace) {  // ZK_DEBUG_TAIL: kernel entry, challenge received, publish per step (block 0 / last block)
+    HIPCK(hipStreamSynchronize(c->stream));
+    const uint64_t* T = c->tail_trace + 512;
+    uint64_t prev_pub = 0;
+    for (size_t si = 0; si < ns; ++si) {
+      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL) break;
+      const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
+      fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f\n", si,
+              steps[si].kind, steps[si].i, prev_pub ? (row[0] - prev_pub) * 0.01 : 0.0,
+              steps[si].kind == GS_ROUND0 ? 0.0 : (row[1] - row[0]) * 0.01,
+              (row[2] - (steps[si].kind == GS_ROUND0 ? row[0] : row[1])) * 0.01);
+      prev_pub = row[2];
+    }
+  }
   if (c->tail_trace && !steps.empty() && steps.back().kind == GS_TAIL) {  // ZK_DEBUG_TAIL
     HIPCK(hipStreamSynchronize(c->stream));
     const uint64_t* T = c->tail_trace;

@@ -109,7 +109,11 @@ struct RoundSink {
   uint64_t* host_out;   // C u64 in pinned host memory, or null
   uint32_t* host_flag;  // pinned host word, or null
   uint32_t tag;
+  uint64_t* trace;      // debug (ZK_DEBUG_TAIL): 4 s_memrealtime stamps per tag (entry, challenge, publish), or null
 };
+// block 0 / the publishing block stamps slot i of this sink's trace row
+#define ZK_SINK_STAMP(sk, i) \
+  do { if ((sk).trace && threadIdx.x == 0) (sk).trace[((sk).tag & 63) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 
 // ---------------------------------------------------------------------------
 // Pre-enqueued rounds. The host enqueues every round kernel up front; round
@@ -258,6 +262,7 @@ __device__ __forceinline__ void publish_limbs(Sc& sc, const RoundSink& sk) {
     if (sk.host_out) __hip_atomic_store(sk.host_out + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ZK_SINK_STAMP(sk, 2);
   if (C > 64) __syncthreads();  // every storing wave has drained before the flag
   if (t == 0 && sk.host_flag) __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -387,6 +392,7 @@ template <class F>
 __global__ __launch_bounds__(kBlock) void k_gkr_round0(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                        const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                        uint64_t h, RoundSink sink) {
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   // products accumulate unreduced (Wide) and are reduced once per thread
   Wide w0 = wide_zero<F>(), w1 = wide_zero<F>(), w2 = wide_zero<F>();
   uint64_t j, step;
@@ -436,7 +442,9 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
                                                       Fe* __restrict__ M2, Fe* __restrict__ P2, uint64_t h,
                                                       RoundIn rin, RoundSink sink) {
   ZK_STAMP(0);
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   const Fe r = block_get_r(rin);
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   Wide w0 = wide_zero<F>(), w2 = wide_zero<F>();
   uint64_t j, step;
   uint32_t q;
@@ -839,7 +847,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
                                                        DIn din, RoundSink sink) {
   static_assert(NP == 1 || NP == 2, "one or two pending challenges");
   Fe ra, rb, rab;
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   block_get_rs(din, ra, rb, rab, gridDim.x > 1);
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ DScratch sc;
   // wave w: product w & 1 (A*S or M*P), quads (w >> 1) * 8 + [0, 8) of each 16; lane = 8 unit + 4 tab + k
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1;

@@ -59,8 +59,8 @@ int zk_ctx_create(int device, zk_ctx** out) {
       HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_red), kHostPage, hipHostMallocMapped | hipHostMallocCoherent));
       memset(c->h_red, 0, kHostPage);
       if (getenv("ZK_DEBUG_TAIL")) {
-        HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->tail_trace), 64 * 8 * 8, hipHostMallocMapped | hipHostMallocCoherent));
-        memset(c->tail_trace, 0, 64 * 8 * 8);
+        HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->tail_trace), 1024 * 8, hipHostMallocMapped | hipHostMallocCoherent));
+        memset(c->tail_trace, 0, 1024 * 8);  // [0, 512): tail kernels, [512, 768): per-step stamps
       }
     } catch (...) {
       zk_ctx_destroy(c);
