@@ -401,4 +401,36 @@ ZK_HD bool fe_is_canonical(const Fe& x) {
   return b != 0;
 }
 
+// 2^e mod p as a plain (non-Montgomery) integer, at compile time (e doublings)
+template <class F>
+constexpr Fe pow2_mod_p(int e) {
+  Fe x{};
+  x.v[0] = 1;
+  for (int i = 0; i < e; ++i) {
+    uint32_t y[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t c = 0;
+    for (int k = 0; k < 8; ++k) {
+      const uint64_t s = ((uint64_t)x.v[k] << 1) | c;
+      y[k] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+    bool ge = true;  // y >= p (y < 2p < 2^256)
+    for (int k = 7; k >= 0; --k)
+      if (y[k] != F::P[k]) {
+        ge = y[k] > F::P[k];
+        break;
+      }
+    if (ge) {
+      uint32_t b = 0;
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t d = (uint64_t)y[k] - F::P[k] - b;
+        y[k] = (uint32_t)d;
+        b = (uint32_t)(d >> 63);
+      }
+    }
+    for (int k = 0; k < 8; ++k) x.v[k] = y[k];
+  }
+  return x;
+}
+
 }  // namespace zk

@@ -62,6 +62,102 @@ __device__ __forceinline__ Fe at2(const Fe& lo, const Fe& hi) {
   return fe_sub<F>(fe_dbl<F>(hi), lo);
 }
 
+// ---------------------------------------------------------------------------
+// Folding by challenges that are constant for a whole step. For a challenge x
+// the block builds, once, the 10 constants c_x[k] = x * 2^(26k + 64) mod p
+// (k = 0..9: `fold_consts`, one Montgomery multiply each by the compile-time
+// K_k = 2^(26k+64) mod p). A product x * d (d a Montgomery image) is then
+//   sum_k d_k c_x[k] = x d 2^64 (mod p), d_k = 26-bit limbs of d,
+// whose eight 32-bit column sums stay below 2^63 even for three challenges
+// at once, so every column is ONE chain of v_mad_u64_u32 with its 64-bit
+// addend (no carry instructions), followed by two 32-bit REDC steps
+// (/2^64: the Montgomery image of x d, < 2p) and one conditional subtraction.
+// 80 + 16 multiply-adds for one fold (fe_mul: 136 plus ~140 carry
+// instructions); 240 + 16 for the three products of fold2.
+// ---------------------------------------------------------------------------
+#define ZK_FOLDK_INIT(F)                                                                                            \
+  {pow2_mod_p<F>(64), pow2_mod_p<F>(90), pow2_mod_p<F>(116), pow2_mod_p<F>(142), pow2_mod_p<F>(168),                 \
+   pow2_mod_p<F>(194), pow2_mod_p<F>(220), pow2_mod_p<F>(246), pow2_mod_p<F>(272), pow2_mod_p<F>(298)}
+static __constant__ Fe kFoldKBn254Fr[10] = ZK_FOLDK_INIT(Bn254Fr);
+static __constant__ Fe kFoldKBn254Fq[10] = ZK_FOLDK_INIT(Bn254Fq);
+static __constant__ Fe kFoldKBls12_381Fr[10] = ZK_FOLDK_INIT(Bls12_381Fr);
+template <class F>
+__device__ __forceinline__ Fe foldk(uint32_t k) {
+  if constexpr (F::id == BN254_FR) return kFoldKBn254Fr[k];
+  else if constexpr (F::id == BN254_FQ) return kFoldKBn254Fq[k];
+  else return kFoldKBls12_381Fr[k];
+}
+// ct[10 x + k] = c_x[k] for the NX challenges xs (Montgomery images); ends with a barrier
+template <class F, int NX>
+__device__ __forceinline__ void fold_consts(const Fe& x0, const Fe& x1, const Fe& x2, Fe (&ct)[NX * 10]) {
+  const uint32_t t = threadIdx.x;
+  if (t < (uint32_t)(NX * 10)) {
+    const uint32_t x = t / 10, k = t % 10;
+    const Fe r = x == 0 ? x0 : (x == 1 ? x1 : x2);
+    ct[t] = fe_mul<F>(r, foldk<F>(k));  // x R K R^-1 = x K
+  }
+  __syncthreads();
+}
+// sum_x d[x] * challenge(OFF + x) mod p (Montgomery images in, fully reduced out)
+template <class F, int NX, int OFF, int NC>
+__device__ __forceinline__ Fe lin_redc(const Fe (&d)[NX], const Fe (&ct)[NC]) {
+  static_assert(OFF + NX <= NC / 10, "constant table too small");
+  uint64_t S[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int x = 0; x < NX; ++x) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int bit = 26 * k, w = bit >> 5, o = bit & 31;
+      const uint32_t lo = d[x].v[w], hi = w + 1 < 8 ? d[x].v[w + 1] : 0u;
+      const uint32_t dk = (o == 0 ? lo : __builtin_amdgcn_alignbit(hi, lo, (uint32_t)o)) & 0x3FFFFFFu;
+      const Fe c = ct[(OFF + x) * 10 + k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) S[j] = (uint64_t)dk * c.v[j] + S[j];
+    }
+  }
+  uint32_t t[10];
+  t[0] = (uint32_t)S[0];
+  uint64_t carry = S[0] >> 32;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) {
+    const uint64_t v = S[j] + carry;
+    t[j] = (uint32_t)v;
+    carry = v >> 32;
+  }
+  t[8] = (uint32_t)carry;
+  t[9] = (uint32_t)(carry >> 32);
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {  // REDC by 2^32, twice
+    const uint32_t m = t[0] * F::PINV;
+    uint64_t Q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Q[j] = mad64(m, F::P[j], t[j]);
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) t[j - 1] = addc32((uint32_t)Q[j], (uint32_t)(Q[j - 1] >> 32), c, &c);
+    t[7] = addc32(t[8], (uint32_t)(Q[7] >> 32), c, &c);
+    t[8] = t[9] + c;
+    t[9] = 0;
+  }
+  Fe r;  // < 2p < 2^256: t[8] == 0
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.v[j] = t[j];
+  return fe_reduce_once<F>(r);
+}
+// a + r (b - a) with r's constants at block OFF of ct
+template <class F, int OFF, int NC>
+__device__ __forceinline__ Fe fold1c(const Fe& a, const Fe& b, const Fe (&ct)[NC]) {
+  const Fe d[1] = {fe_sub<F>(b, a)};
+  return fe_add<F>(a, lin_redc<F, 1, OFF>(d, ct));
+}
+// fold2 (field.hpp) with the constants of (ra, rb, ra rb) at blocks 0, 1, 2 of ct
+template <class F, int NC>
+__device__ __forceinline__ Fe fold2c(const Fe& x00, const Fe& x01, const Fe& x10, const Fe& x11, const Fe (&ct)[NC]) {
+  const Fe d1 = fe_sub<F>(x10, x00), d2 = fe_sub<F>(x01, x00);
+  const Fe d[3] = {d1, d2, fe_sub<F>(fe_sub<F>(x11, x01), d1)};
+  return fe_add<F>(x00, lin_redc<F, 3, 0>(d, ct));
+}
+
 // Where a round kernel's sums go. Everything after the main loop is integer
 // work: a thread's accumulators (17-word unreduced product sums `Wide`, or
 // 8-word element sums `Fe`) are summed over the block column by column
@@ -432,6 +528,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_round0(const Fe* __restrict__ A,
 #ifndef ZK_ROUND_WAVES
 #define ZK_ROUND_WAVES 1
 #endif
+#ifndef ZK_ROUND_FOLDC  // round 1 folds with the per-block constant tables (1) or fe_mul (0)
+#define ZK_ROUND_FOLDC 1
+#endif
 #ifndef ZK_ROUND_LOADS_FIRST
 #define ZK_ROUND_LOADS_FIRST 1
 #endif
@@ -445,6 +544,10 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   const Fe r = block_get_r(rin);
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
+#if ZK_ROUND_FOLDC
+  __shared__ Fe ct[10];
+  fold_consts<F, 1>(r, r, r, ct);
+#endif
   Wide w0 = wide_zero<F>(), w2 = wide_zero<F>();
   uint64_t j, step;
   uint32_t q;
@@ -459,8 +562,13 @@ __global__ __launch_bounds__(kBlock, ZK_ROUND_WAVES) void k_gkr_round(const Fe* 
 #if ZK_ROUND_LOADS_FIRST
     __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
 #endif
+#if ZK_ROUND_FOLDC
+    const Fe a0 = fold1c<F, 0>(x0, x2, ct), a1 = fold1c<F, 0>(x1, x3, ct);
+    const Fe s0 = fold1c<F, 0>(z0, z2, ct), s1 = fold1c<F, 0>(z1, z3, ct);
+#else
     const Fe a0 = fold1<F>(x0, x2, r), a1 = fold1<F>(x1, x3, r);
     const Fe s0 = fold1<F>(z0, z2, r), s1 = fold1<F>(z1, z3, r);
+#endif
     st_fold(X2, j, a0);
     st_fold(X2, j + h, a1);
     st_fold(Z2, j, s0);
@@ -850,6 +958,11 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   block_get_rs(din, ra, rb, rab, gridDim.x > 1);
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
+  __shared__ Fe ct[NP == 2 ? 30 : 10];  // fold constants of (ra, rb, ra rb) or rb
+  if constexpr (NP == 2)
+    fold_consts<F, NP == 2 ? 3 : 1>(ra, rb, rab, ct);
+  else
+    fold_consts<F, NP == 2 ? 3 : 1>(rb, rb, rb, ct);
   __shared__ DScratch sc;
   // wave w: product w & 1 (A*S or M*P), quads (w >> 1) * 8 + [0, 8) of each 16; lane = 8 unit + 4 tab + k
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1;
@@ -863,14 +976,14 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
     if (j < Q) {  // uniform over the 8 lanes of a unit
       const uint64_t i = j + k * Q;
       Fe z;
-      if (NP == 2) {
+      if constexpr (NP == 2) {
         const Fe x00 = ld_fe(X, i), x01 = ld_fe(X, i + h4), x10 = ld_fe(X, i + 2 * h4), x11 = ld_fe(X, i + 3 * h4);
         __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
-        z = fold2<F>(x00, x01, x10, x11, ra, rb, rab);
+        z = fold2c<F>(x00, x01, x10, x11, ct);
       } else {
         const Fe x0 = ld_fe(X, i), x1 = ld_fe(X, i + h4);
         __builtin_amdgcn_sched_barrier(0);
-        z = fold1<F>(x0, x1, rb);
+        z = fold1c<F, 0>(x0, x1, ct);
       }
       st_fold(X2, i, z);
       unit_product<F>(z, k, tab, acc);
@@ -914,6 +1027,7 @@ __host__ __device__ __forceinline__ uint64_t dtail_region(uint64_t Q0, uint32_t 
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sink) {
   __shared__ DScratch sc;
+  __shared__ Fe ct[30];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1;
   const uint32_t pp = wv & 1, jl = (wv >> 1) * 8 + (lane >> 3);
   const uint32_t tb = 2 * pp + tab;  // table A, S, M, P
@@ -932,6 +1046,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     block_get_rs(din, ra, rb, rab, nb > 1);
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 1] = __builtin_amdgcn_s_memrealtime();
     const bool two = st > 0 || a.np0 == 2;
+    fold_consts<F, 3>(ra, rb, rab, ct);  // blocks 0, 1, 2: ra, rb, ra rb
     const uint64_t h4 = 4 * Q;
     const Fe* X;
     if (st == 0) {
@@ -946,8 +1061,8 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
       const uint64_t j = jb + jl;
       if (j < Q) {
         const uint64_t i = j + k * Q;
-        const Fe z = two ? fold2<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ld_fe_a(X, i + 2 * h4), ld_fe_a(X, i + 3 * h4), ra, rb, rab)
-                         : fold1<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), rb);
+        const Fe z = two ? fold2c<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ld_fe_a(X, i + 2 * h4), ld_fe_a(X, i + 3 * h4), ct)
+                         : fold1c<F, 1>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ct);
         st_fe_a(X2, i, z);
         unit_product<F>(z, k, tab, acc);
       }
