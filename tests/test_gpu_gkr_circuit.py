@@ -50,6 +50,32 @@ def test_reference_circuit(ctx):  # gkr_protocol.rs:473-506
     assert verify(got, circ, inputs)
 
 
+@pytest.mark.parametrize("field", [0, 1, 2])
+def test_two_phase_equals_dense_tables(monkeypatch, field):
+    """The default layer prover (two phases over tables of L = 2G entries) and
+    ZK_CIRCUIT_DENSE=1 (the four L^2 tables, then the generic sum-check) give
+    the same proof on a 2^10-input circuit (input layer: 20 sum-check rounds)."""
+    import zk_amd
+
+    rng = random.Random(5 + field)
+    depth = 10
+    structure = [[rng.choice((Operation.Add, Operation.Mul)) for _ in range(1 << (depth - 1 - i))] for i in range(depth)]
+    p = go.MODULI[field]
+    inputs = [rng.randrange(p) for _ in range(1 << depth)]
+    circ = Circuit(structure, field)
+    proofs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("ZK_CIRCUIT_DENSE", mode)
+        c = zk_amd.Context(0)
+        try:
+            pr = prove(circ, inputs, c)
+            proofs[mode] = ([[q.coefficient for q in layer] for layer in pr.proof_polynomials], pr.claimed_evaluations,
+                            pr.input_evaluations, pr.output_poly)
+        finally:
+            c.close()
+    assert proofs["0"] == proofs["1"]
+
+
 @pytest.mark.parametrize("field", [0, 2])
 def test_large_circuit_verifies(ctx, field):
     rng = random.Random(77 + field)

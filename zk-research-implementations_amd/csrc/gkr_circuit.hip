@@ -56,6 +56,47 @@ struct CircuitOut {
   Fe in_eval[2];
 };
 
+// One layer's sum-check (2 lgL rounds) in two phases over tables of L = 2^lgL
+// entries (kernels.hpp k_phase1_tables / k_phase2_tables): the same round
+// polynomials and challenges as gkr_prove over the dense L^2 tables, since
+// every round value is the same field sum. Phase 1 binds b (rounds 0 .. lgL-1),
+// w(r_b) is evaluated on the device, phase 2 binds c; both phases run the
+// device sum-check of the hot path (gkr_phase) on the shared transcript.
+template <class F>
+void gkr_layer_two_phase(zk_ctx* c, const Fe* w, const Fe* wt, const uint8_t* ops, uint32_t lgL, zk_transcript* tr,
+                         GkrOut& out) {
+  const uint32_t nv = 2 * lgL;
+  const uint64_t L = (uint64_t)1 << lgL;
+  out.coeffs.assign(3 * (size_t)nv, zk::fe_zero<F>());
+  out.ncoeffs.assign(nv, 0);
+  out.challenges.assign(nv, zk::fe_zero<F>());
+  ensure_partials(c);
+  __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
+  c->work[0].ensure(4 * std::max<uint64_t>(L / 2, 1) * 32);
+  c->work[1].ensure(4 * std::max<uint64_t>(L / 4, 1) * 32);
+  c->input.ensure(8 * L * 32);
+  Fe* t1 = c->input.fe();
+  Fe* t2 = t1 + 4 * L;
+  const uint32_t blocks = (uint32_t)((L + zk::kBlock - 1) / zk::kBlock);
+  launch(c, ZK_K_LAYER, 160.0 * L, 0.5 * L, zk::k_phase1_tables<F>, blocks, w, wt, ops, (uint32_t)L, t1, t1 + L,
+         t1 + 2 * L, t1 + 3 * L);
+  const Fe* cur[4] = {t1, t1 + L, t1 + 2 * L, t1 + 3 * L};
+  Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
+  uint32_t pend = 0;
+  gkr_phase<F>(c, cur, lgL, 0, false, tr, out, claim, r, pend);  // rounds 0 .. lgL-1 (b)
+  zk::LayerPts ep{};  // w(r_b) in both slots of the two-point evaluation
+  for (uint32_t k = 0; k < lgL; ++k) ep.r[k] = ep.r[lgL + k] = out.challenges[k];
+  const zk::RoundSink sk = make_sink(c, false);
+  launch(c, ZK_K_LAYER, 32.0 * L, 4.0 * L, zk::k_mle_eval2<F>, grid_for(c, L, zk::k_mle_eval2<F>), w, lgL, ep, sk);
+  Fe ev[2];
+  collect_sums<F, 2>(c, sk, false, 17, ev);
+  launch(c, ZK_K_LAYER, 160.0 * L, (double)L * (lgL + 2), zk::k_phase2_tables<F>, blocks, w, wt, ops, lgL, ep, ev[0],
+         t2, t2 + L, t2 + 2 * L, t2 + 3 * L);
+  const Fe* cur2[4] = {t2, t2 + L, t2 + 2 * L, t2 + 3 * L};
+  gkr_phase<F>(c, cur2, lgL, lgL, false, tr, out, claim, r, pend);  // rounds lgL .. 2 lgL-1 (c)
+  sync(c);
+}
+
 template <class F>
 void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
                               const zk_fe* inputs, uint32_t ninputs, CircuitOut& o) {
@@ -135,18 +176,23 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     std::copy(pts.begin(), pts.end(), lp.r);
     launch(c, ZK_K_LAYER, 32.0 * G, (double)G * (W + 2), k_gate_weights<F>, (G + kBlock - 1) / kBlock, lp, W, a, b,
            has_c, G, dwt.b.fe(0));
-    c->input.ensure(4 * T * 32);
-    Fe* tab = c->input.fe();
-    const uint32_t grid = grid_for(c, T, k_layer_tables<F>);
-    launch(c, ZK_K_LAYER, 128.0 * T, (double)T, k_layer_tables<F>, grid, w, lgL, dwt.b.fe(0), dop + opoff[l], tab,
-           tab + T, tab + 2 * T, tab + 3 * T);
-    const Fe* dT[4] = {tab, tab + T, tab + 2 * T, tab + 3 * T};
-    if (dbg) {
-      sync(c);
-      t1 = clk::now();
-    }
     GkrOut g;
-    gkr_prove_device<F>(c, dT, nv, false, &tr, g);  // gkr_prove(claimed_sum, &fbc_poly, &mut transcript) (:68)
+    if (c->circuit_dense) {  // ZK_CIRCUIT_DENSE=1: the four L^2 tables, then the generic sum-check
+      c->input.ensure(4 * T * 32);
+      Fe* tab = c->input.fe();
+      const uint32_t grid = grid_for(c, T, k_layer_tables<F>);
+      launch(c, ZK_K_LAYER, 128.0 * T, (double)T, k_layer_tables<F>, grid, w, lgL, dwt.b.fe(0), dop + opoff[l], tab,
+             tab + T, tab + 2 * T, tab + 3 * T);
+      const Fe* dT[4] = {tab, tab + T, tab + 2 * T, tab + 3 * T};
+      if (dbg) {
+        sync(c);
+        t1 = clk::now();
+      }
+      gkr_prove_device<F>(c, dT, nv, false, &tr, g);  // gkr_prove(claimed_sum, &fbc_poly, &mut transcript) (:68)
+    } else {  // two phases over tables of size L (kernels.hpp k_phase1_tables / k_phase2_tables)
+      if (dbg) t1 = clk::now();
+      gkr_layer_two_phase<F>(c, w, dwt.b.fe(0), dop + opoff[l], lgL, &tr, g);
+    }
     if (dbg) t2 = clk::now();
     for (uint32_t k = 0; k < nv; ++k) {
       for (int i = 0; i < 3; ++i) o.sc.coeffs[3 * (size_t)(k0 + k) + i] = g.coeffs[3 * (size_t)k + i];

@@ -1281,6 +1281,68 @@ __global__ __launch_bounds__(kBlock) void k_layer_tables(const Fe* __restrict__ 
   }
 }
 
+// The same layer sum-check from tables of size L instead of L^2 (two phases,
+// the linear-time GKR prover of Thaler / Libra). Variables 0 .. lgL-1 are the
+// bits of b (MSB first), lgL .. 2 lgL - 1 those of c. With A(b, c) and M(b, c)
+// nonzero only at (2g, 2g+1) and S = w(b) + w(c), P = w(b) w(c):
+//   phase 1 (b):  sum_c [A S + M P](b, c) = W(b) U(b) + V(b) 1, with
+//     W = w, U(2g) = wt_g (add) or wt_g w(2g+1) (mul), V(2g) = wt_g w(2g+1)
+//     (add), U = V = 0 at odd b;
+//   phase 2 (c), b bound to r_b:  A(r_b, 2g+1) = wt_g eq(r_b, 2g) (add),
+//     M likewise (mul), S = w(r_b) + w(c), P = w(r_b) w(c).
+// Every table is linear in the variable being folded, so each round's e0, e1,
+// e2 equal the dense tables' (the same field values, hence the same proof).
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_phase1_tables(const Fe* __restrict__ w, const Fe* __restrict__ wt,
+                                                          const uint8_t* __restrict__ ops, uint32_t L,
+                                                          Fe* __restrict__ W, Fe* __restrict__ U,
+                                                          Fe* __restrict__ V, Fe* __restrict__ ONE) {
+  const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+  if (b >= L) return;
+  const Fe wb = ld_fe(w, b);
+  Fe u = fe_zero<F>(), v = fe_zero<F>();
+  if ((b & 1u) == 0) {
+    const Fe x = ld_fe(wt, b >> 1), xw = fe_mul<F>(x, ld_fe(w, b + 1));
+    if (ops[b >> 1]) {
+      u = xw;
+    } else {
+      u = x;
+      v = xw;
+    }
+  }
+  st_fe(W, b, wb);
+  st_fe(U, b, u);
+  st_fe(V, b, v);
+  st_fe(ONE, b, fe_one<F>());
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_phase2_tables(const Fe* __restrict__ w, const Fe* __restrict__ wt,
+                                                          const uint8_t* __restrict__ ops, uint32_t lgL,
+                                                          const LayerPts rb /* lgL coordinates */, Fe wrb,
+                                                          Fe* __restrict__ A, Fe* __restrict__ S,
+                                                          Fe* __restrict__ M, Fe* __restrict__ P) {
+  const uint32_t L = 1u << lgL, c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= L) return;
+  const Fe wc = ld_fe(w, c);
+  Fe a = fe_zero<F>(), m = fe_zero<F>();
+  if (c & 1u) {
+    const uint32_t b = c - 1;  // the gate's left input
+    const Fe one = fe_one<F>();
+    Fe e = ld_fe(wt, b >> 1);
+    for (uint32_t k = 0; k < lgL; ++k) {
+      const Fe rk = rb.r[k];
+      e = fe_mul<F>(e, ((b >> (lgL - 1 - k)) & 1u) ? rk : fe_sub<F>(one, rk));
+    }
+    if (ops[b >> 1]) m = e;
+    else a = e;
+  }
+  st_fe(A, c, a);
+  st_fe(S, c, fe_add<F>(wrb, wc));
+  st_fe(M, c, m);
+  st_fe(P, c, fe_mul<F>(wrb, wc));
+}
+
 // Both evaluations w.evaluate(r_b), w.evaluate(r_c) of a layer's input table
 // (gkr_protocol.rs:75-76) in one pass. evaluate folds variable 0 (the MSB)
 // first, so w(r) = sum_j w[j] eq(r, j) with eq MSB-first; eq splits into the
