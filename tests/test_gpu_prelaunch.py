@@ -5,7 +5,9 @@
   each round after its challenge), and equal to the oracle's.
 * From round 2 on two rounds run per kernel (k_gkr_dround, default); the
   proof is identical with one round per kernel (ZK_DROUND=0), for odd and
-  even round counts, pre-enqueued or not.
+  even round counts, pre-enqueued or not. With ZK_D0=1 (off by default:
+  measured slower) even counts run rounds 0 and 1 in one pass over the
+  inputs (k_gkr_d0); the proof is identical.
 * The small double steps run in one persistent kernel (k_gkr_dtail, default);
   the proof is identical with one launch per step (ZK_DTAIL=0), when it
   starts at the first double step over large tables (ZK_DTAIL_MAX_QUADS) and
@@ -118,11 +120,44 @@ def test_double_and_single_rounds_agree_20var(monkeypatch, field):
     assert got["1"] == got["0"]
 
 
+@pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("n", [2, 4, 8, 16])
+def test_first_double_step_matches_oracle(monkeypatch, field, n):
+    """With ZK_D0=1 even variable counts start with rounds 0 and 1 in one pass
+    over the inputs (k_gkr_d0: nine product sums, nothing written); ZK_D0=0
+    runs round 0 alone and round 1 as a single step. Both equal the oracle, pre-enqueued
+    and per-round launched."""
+    want = _oracle(field, n)
+    for d0 in ("1", "0"):
+        for pre in ("1", "0"):
+            monkeypatch.setenv("ZK_D0", d0)
+            monkeypatch.setenv("ZK_PRELAUNCH", pre)
+            ctx = zk_amd.Context(0)
+            try:
+                assert _prove(ctx, field, n) == want, f"ZK_D0={d0} ZK_PRELAUNCH={pre}"
+            finally:
+                ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 2])
+def test_first_double_step_agrees_22var(monkeypatch, field):
+    n = 22
+    got = {}
+    for d0 in ("1", "0"):
+        monkeypatch.setenv("ZK_D0", d0)
+        ctx = zk_amd.Context(0)
+        try:
+            got[d0] = _prove(ctx, field, n)
+        finally:
+            ctx.close()
+    assert got["1"] == got["0"]
+
+
 @pytest.mark.parametrize("field", [0, 2])
 @pytest.mark.parametrize("env", [{"ZK_DTAIL": "0"}, {"ZK_DTAIL_MAX_QUADS": str(1 << 16)}, {"ZK_DTAIL_BLOCKS": "1"},
                                  {"ZK_DTAIL_MAX_QUADS": "16"}])
-def test_dtail_modes_agree(monkeypatch, field, env):
-    n = 17
+@pytest.mark.parametrize("n", [16, 17])
+def test_dtail_modes_agree(monkeypatch, field, env, n):
     want = _oracle(field, n)
     for key, val in env.items():
         monkeypatch.setenv(key, val)

@@ -59,9 +59,12 @@ def _oracle(field: int, n: int) -> dict:
             "blob_keccak": po.keccak256(po.proof_blob(po.BLOB_GKR, field, 0, [list(p) for p in polys])).hex()}
 
 
-def _steps(nloc: int) -> int:
+def _steps(nloc: int, d0: bool = False) -> int:
     """Kernel steps of a phase of nloc rounds, one all-reduce each: round 0,
-    round 1, one more single round if nloc - 2 is odd, then two rounds per step."""
+    round 1, one more single round if nloc - 2 is odd, then two rounds per step.
+    With ZK_D0=1 an even phase runs rounds 0 and 1 in one step."""
+    if d0 and nloc % 2 == 0:
+        return nloc // 2
     if nloc <= 2:
         return nloc
     return 2 + (nloc - 2) % 2 + (nloc - 2) // 2
@@ -90,3 +93,17 @@ def test_rccl_data_path_forced_at_world1(tmp_path):
     want = _oracle(0, 14)
     assert {"polys": res[0]["polys"], "chal": res[0]["chal"], "blob_keccak": res[0]["blob_keccak"]} == want
     assert res[0]["collectives"] == _steps(14)  # every step went through ncclAllReduce
+
+
+@pytest.mark.parametrize("comm,world,nloc", [("host", 2, 10), ("rccl", 1, 12)])
+def test_first_double_step_sharded(tmp_path, comm, world, nloc):
+    """ZK_D0=1 (rounds 0 and 1 in one step over the inputs): its nine limb
+    sums go through the same all-reduce as every other step."""
+    env = {"ZK_D0": "1"}
+    if comm == "rccl":
+        env["ZK_FORCE_COLLECTIVES"] = "1"
+    res = _run(world, comm, 0, nloc, str(tmp_path), env)
+    want = _oracle(0, nloc + world.bit_length() - 1)
+    for rank, r in enumerate(res):
+        assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
+        assert r["collectives"] == _steps(nloc, d0=True) + (1 if world > 1 else 0)

@@ -202,6 +202,7 @@ struct zk_ctx {
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
+  bool d0 = false;          // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0=1; measured slower)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
@@ -516,7 +517,7 @@ struct GStep {
   int np;          // double / dtail: pending challenges at entry (1 or 2)
   uint32_t nd = 0; // dtail: double steps it runs
 };
-enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4 };
+enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5 };
 
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
@@ -524,12 +525,16 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   const uint64_t L = (uint64_t)1 << nv;
   const bool pre = prelaunch(c, nv);
   std::vector<GStep> steps;
-  if (nv >= 1) steps.push_back({GS_ROUND0, 0, 0});
+  const bool d0 = c->dround && c->d0 && nv >= 2 && nv % 2 == 0;  // rounds 0 and 1 in one pass over the inputs
+  if (nv >= 1) steps.push_back({d0 ? GS_D0 : GS_ROUND0, 0, 0});
   if (c->dround) {
-    uint32_t i = 1;
-    if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
-    if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
-    for (int np = 1; i + 1 < nv; i += 2, np = 2) steps.push_back({GS_DOUBLE, i, np});
+    uint32_t i = d0 ? 2 : 1;
+    int np = d0 ? 2 : 1;  // challenges pending at the first double step
+    if (!d0) {
+      if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
+      if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
+    }
+    for (; i + 1 < nv; i += 2, np = 2) steps.push_back({GS_DOUBLE, i, np});
     // the small doubles (>= 2 of them) in one persistent kernel
     if (pre && c->dtail && use_tail(c, across_ranks)) {
       size_t d0 = 0;
@@ -588,6 +593,13 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round0<F>);
       launch(c, ZK_K_GKR_ROUND0, 256.0 * h, 6.0 * h, zk::k_gkr_round0<F>, grid, cur[0], cur[1], cur[2], cur[3], h, sk);
       enqueue_reduce(c, sk, across_ranks, 3 * 17);
+      return;
+    }
+    if (st.kind == GS_D0) {  // rounds 0 and 1 over the input tables (size 4Q), nothing written
+      const uint64_t Q = size / 4;
+      const uint32_t grid = grid_for(c, zk::kDQuads * Q, zk::k_gkr_d0<F>);
+      launch(c, ZK_K_GKR_ROUND0, 128.0 * size, 4.5 * size, zk::k_gkr_d0<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
+      enqueue_reduce(c, sk, across_ranks, zk::kD0Limbs);
       return;
     }
     if (st.kind == GS_TAIL) {
@@ -734,14 +746,22 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     ra = rb;
     rb = r;
   };
-  // rounds i0 and i0 + 1 from a double step's eight product sums
-  auto two_rounds = [&](uint32_t i0) {
-      Fe d[zk::kDCats];
-      collect_sums<F, zk::kDCats>(c, sinks[i0], across_ranks, 17, d);
-      // categories: 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21, 7 V12 (kernels.hpp)
-      // round i: e0 = V00 + V01, e2 = V20 + V21
+  // rounds i0 and i0 + 1 from a double step's eight product sums (the first
+  // step of a phase, k_gkr_d0: nine, the ninth V11 for round 0's e1)
+  auto two_rounds = [&](uint32_t i0, bool first = false) {
+      Fe d[zk::kD0Cats];
+      if (first)
+        collect_sums<F, zk::kD0Cats>(c, sinks[i0], across_ranks, 17, d);
+      else {
+        Fe d8[zk::kDCats];
+        collect_sums<F, zk::kDCats>(c, sinks[i0], across_ranks, 17, d8);
+        std::copy(d8, d8 + zk::kDCats, d);
+      }
+      // categories: 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21, 7 V12, 8 V11 (kernels.hpp)
+      // round i: e0 = V00 + V01, e1 = V10 + V11 (first) or s_{i-1}(r_{i-1}) - e0, e2 = V20 + V21
       const Fe e0 = zk::hfe_add<F>(d[0], d[2]);
-      one_round(i0, e0, zk::hfe_sub<F>(claim, e0), zk::hfe_add<F>(d[5], d[6]));
+      const Fe e1 = first ? zk::hfe_add<F>(d[4], d[8]) : zk::hfe_sub<F>(claim, e0);
+      one_round(i0, e0, e1, zk::hfe_add<F>(d[5], d[6]));
       // round i + 1 at r = r_i: e0' through (V00, V10, V20), e2' through (V02, V12, V22) at r = 0, 1, 2
       const Fe one = zk::fe_one<F>(), two = zk::hfe_add<F>(one, one), h = zk::fe_inv2<F>();
       const Fe rm1 = zk::hfe_sub<F>(r, one), rm2 = zk::hfe_sub<F>(r, two);
@@ -762,6 +782,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       collect_sums<F, 3>(c, sinks[0], across_ranks, 17, s3);
       one_round(0, s3[0], s3[1], s3[2]);
       pend = 1;
+    } else if (st.kind == GS_D0) {
+      two_rounds(0, true);
+      pend = 2;
     } else if (st.kind == GS_SINGLE) {
       Fe s2[2];
       collect_sums<F, 2>(c, sinks[st.i], across_ranks, 17, s2);
@@ -795,10 +818,10 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     for (size_t si = 0; si < ns; ++si) {
       if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
+      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0;  // no challenge to wait for
       fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f\n", si,
               steps[si].kind, steps[si].i, prev_pub ? (row[0] - prev_pub) * 0.01 : 0.0,
-              steps[si].kind == GS_ROUND0 ? 0.0 : (row[1] - row[0]) * 0.01,
-              (row[2] - (steps[si].kind == GS_ROUND0 ? row[0] : row[1])) * 0.01);
+              first ? 0.0 : (row[1] - row[0]) * 0.01, (row[2] - (first ? row[0] : row[1])) * 0.01);
       prev_pub = row[2];
     }
   }

@@ -994,6 +994,85 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
 }
 
 // ---------------------------------------------------------------------------
+// Rounds 0 and 1 from the input tables in one pass (even round counts). With
+// nothing to fold, the quad's corners are the inputs themselves; round 0 needs
+// e0 = sum V00^2 + V01^2, e1 = sum V10^2 + V11^2, e2 = sum V20^2 + V21^2 and
+// round 1 the two quadratics through V(.,0) and V(.,2): all nine grid points,
+// the eight of k_gkr_dround plus the corner V11 (category 8). Its product is
+// split over the unit's 8 lanes, lane u = 4 tab + k forming schoolbook row u
+// (V11_A times word u of V11_S); the row sums are shifted by u words when the
+// block sums them (d0_limb_sums). Nothing is written: the next step folds the
+// inputs by (r_0, r_1) at once.
+// ---------------------------------------------------------------------------
+constexpr int kD0Cats = 9;
+constexpr int kD0Limbs = kD0Cats * 17;  // 153 limb sums
+struct D0Scratch {
+  uint32_t rows[kBlock * 27];  // 17 words of the eight-point accumulator + 10 of the row accumulator
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+};
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_gkr_d0(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                   const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t Q,
+                                                   RoundSink sink) {
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  __shared__ D0Scratch sc;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1, u = lane & 7;
+  const uint32_t pp = wv & 1, jl = (wv >> 1) * 8 + (lane >> 3);
+  const Fe* __restrict__ X = pp ? (tab ? P : M) : (tab ? S : A);
+  Wide acc = wide_zero<F>();
+  uint32_t row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // sum of this lane's schoolbook rows of V11_A V11_S
+  for (uint64_t jb = (uint64_t)blockIdx.x * kDQuads; jb < Q; jb += (uint64_t)gridDim.x * kDQuads) {
+    const uint64_t j = jb + jl;
+    if (j < Q) {  // uniform over the 8 lanes of a unit
+      const Fe q = ld_fe(X, j + k * Q);
+      unit_product<F>(q, k, tab, acc);
+      const Fe own3 = dpp_fe<kQP3333>(q), other3 = xor4_fe(own3);  // V11 of this table, of the other
+      const Fe xa = tab ? other3 : own3, ys = tab ? own3 : other3;  // A side, S side
+      uint32_t yu = ys.v[0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) yu = u == (uint32_t)w ? ys.v[w] : yu;
+      uint64_t Pw[8];
+#pragma unroll
+      for (int w = 0; w < 8; ++w) Pw[w] = (uint64_t)xa.v[w] * yu;
+      uint32_t prod[9], c = 0;  // the 288-bit row, then row += prod
+      prod[0] = (uint32_t)Pw[0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) prod[w] = addc32((uint32_t)Pw[w], (uint32_t)(Pw[w - 1] >> 32), c, &c);
+      prod[8] = (uint32_t)(Pw[7] >> 32) + c;
+      c = 0;
+#pragma unroll
+      for (int w = 0; w < 9; ++w) row[w] = addc32(row[w], prod[w], c, &c);
+      row[9] += c;
+    }
+  }
+  // limb sums: categories 0..7 as k_gkr_dround; category 8 = sum over lanes of row << 32 u
+#pragma unroll
+  for (int w = 0; w < 17; ++w) sc.rows[threadIdx.x * 27 + w] = acc.w[w];
+#pragma unroll
+  for (int w = 0; w < 10; ++w) sc.rows[threadIdx.x * 27 + 17 + w] = row[w];
+  __syncthreads();
+  const uint32_t t = threadIdx.x;
+  if (t < (uint32_t)kDLimbs) {
+    const uint32_t c = t / 17, w = t % 17, uu = 4 * (c & 1) + (c >> 1);
+    uint64_t s0 = 0;
+    for (uint32_t m = 0; m < kBlock / 8; ++m) s0 += sc.rows[(8 * m + uu) * 27 + w];
+    sc.tot[t] = s0;
+  } else if (t < (uint32_t)kD0Limbs) {
+    const uint32_t w = t - kDLimbs;  // column w of category 8
+    uint64_t s0 = 0;
+    for (uint32_t r = 0; r < (uint32_t)kBlock; ++r) {
+      const int src = (int)w - (int)(r & 7u);
+      if (src >= 0 && src < 10) s0 += sc.rows[r * 27 + 17 + src];
+    }
+    sc.tot[t] = s0;
+  }
+  __syncthreads();
+  grid_finish<kD0Limbs>(sc, sink);
+}
+
+// ---------------------------------------------------------------------------
 // The small double rounds of a proof in ONE persistent kernel: step s is the
 // k_gkr_dround step over Q0 >> 2s quads (two pending challenges, the first
 // step np0), run by min(gridDim, Q/16) blocks. The instruction cache stays
