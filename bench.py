@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-fast-nvars", type=int, default=24, help="size of the OpenMP CPU restatement run")
     ap.add_argument("--no-circuit", action="store_true", help="skip the full GKR circuit prove (SURVEY 8(f2))")
     ap.add_argument("--no-config5", action="store_true", help="skip BLS12-381 GKR + KZG commit (BASELINE config 5)")
+    ap.add_argument("--no-config4", dest="config4", action="store_false",
+                    help="skip the 26-variable-total proof split over all ranks (BASELINE config 4, strong scaling)")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
     return ap.parse_args()
 
@@ -276,6 +278,58 @@ def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
     }
 
 
+def config4_bench(ctx, field: int, world: int, rank: int, barrier, total_nvars: int = 26, reps: int = 5) -> dict:
+    """BASELINE config 4 exactly: one gkr_prove over `total_nvars` variables
+    in total, the hypercube split over all ranks (each holds 2^(total - log2 G)
+    elements per table; strong scaling, beside the weak-scaling headline).
+    Every rank calls it (the proof runs the per-round all-reduce); max over
+    ranks of the median per-proof time, barrier-bracketed."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+    from zk_amd.elems import as_limbs, ptr
+
+    lg = (world - 1).bit_length()
+    nloc = total_nvars - lg
+    tabs = [ctx.synth(field, 1 << nloc, seed=4, table=t, index0=rank, stride=world) for t in range(4)]
+    arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
+    coeffs = np.zeros((total_nvars, 3, 4), np.uint64)
+    nco = np.zeros(total_nvars, np.uint8)
+    ch = np.zeros((total_nvars, 4), np.uint64)
+    zero = ptr(as_limbs([0]))
+    times = []
+    for i in range(reps + 1):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tr = zk_amd.Transcript(field)
+        check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, nloc, 0, zero, tr.h, ptr(coeffs), ptr(nco),
+                                                      ptr(ch)))
+        torch.cuda.synchronize()
+        if i:
+            times.append(time.perf_counter() - t0)
+    for t in tabs:
+        t.free()
+    times.sort()
+    med = times[len(times) // 2]
+    if world > 1:
+        t = torch.tensor([med], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        med = float(t.item())
+    return {
+        "workload": f"gkr_prove over {total_nvars} variables total ({nloc} per GPU), seed 4, split over {world} GPU(s)",
+        "scaling": "strong",
+        "ms_median": med * 1e3,
+        "field_ops_per_s": 32.0 * ((1 << total_nvars) - 1) / med,
+        "challenge0_lo": int(ch[0, 0]),
+    }
+
+
 def main() -> None:
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -393,6 +447,7 @@ def main() -> None:
         if t.get("kernel") == "k_gkr_round" and field == 0:  # per-symbol summary of this workload
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
             traffic_src = f"profiles/r1_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
+    cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
     if rank == 0:
         out = {
             "metric": "GKR sum-check field-ops/sec + prover ms, 24-var BN254, 1/2/4/8 GPU",
@@ -444,6 +499,8 @@ def main() -> None:
                 "launches_by_kind": {kk: v["launches"] / args.steps for kk, v in k.items() if v["launches"]},
             },
         }
+        if cfg4 is not None:
+            out["config4_26var"] = cfg4
         if not args.no_e2e and world == 1:
             e2e = e2e_bench(ctx, field, tabs, n)
             e2e["same_proof_as_device_resident"] = bool(np.array_equal(e2e.pop("challenges"), ch))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 7u
+#define ZK_ABI_VERSION 8u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -119,6 +119,21 @@ int zk_mle_partial_evaluate(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_
 /* evaluate(values) :79-91; npoint must equal nvars (else ZK_EINVAL, the panic at :80-82) */
 int zk_mle_evaluate(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
                     const zk_fe* point, uint32_t npoint, zk_fe* out);
+
+/* Table builders (multilinear_polynomial_evaluation.rs): op = ZK_MLE_ADD / MUL / SUB.
+ *   zk_mle_binop   impl Add / Mul / Sub for MultilinearPoly :113-151 — element-wise over the
+ *                  zip of a (2^nvars_a) and b (2^nvars_b): out has 2^min(nvars_a, nvars_b)
+ *   zk_mle_scale   scale(value) :93-97 — out[i] = evals[i] * value, 2^nvars outputs
+ *   zk_mle_tensor  tensor_add_mul_polynomials(a, b, op) :99-110 — out[i nb + j] = op(a[i], b[j]),
+ *                  op ADD or MUL only (Operation :4-17); na * nb must be a nonzero power of
+ *                  two (MultilinearPoly::new panics otherwise) — ZK_EINVAL */
+typedef enum { ZK_MLE_ADD = 0, ZK_MLE_MUL = 1, ZK_MLE_SUB = 2 } zk_mle_op;
+int zk_mle_binop(zk_ctx* ctx, zk_field field, zk_repr repr, zk_mle_op op, const zk_fe* a, uint32_t nvars_a,
+                 const zk_fe* b, uint32_t nvars_b, zk_fe* out);
+int zk_mle_scale(zk_ctx* ctx, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
+                 const zk_fe* value, zk_fe* out);
+int zk_mle_tensor(zk_ctx* ctx, zk_field field, zk_repr repr, zk_mle_op op, const zk_fe* a, uint64_t na,
+                  const zk_fe* b, uint64_t nb, zk_fe* out);
 
 /* ---------------------------------------------------------------------------
  * Sum-check — sum_check/src/sum_check_protocol.rs
@@ -284,6 +299,10 @@ int zk_dev_synth_fill(zk_ctx* ctx, zk_field field, void* dev, uint64_t count, ui
 /* partial_evaluate on device buffers: d_out has 2^(nvars-1) elements (may not alias d_in) */
 int zk_dev_mle_partial_evaluate(zk_ctx* ctx, zk_field field, const void* d_in, uint32_t nvars, uint32_t bit,
                                 zk_repr repr, const zk_fe* value, void* d_out);
+/* tensor_add_mul_polynomials on device buffers (Montgomery): d_out[i nb + j] = op(d_a[i], d_b[j]);
+ * the GKR-shaped S = w (+) w and P = w (x) w tables built in HBM (d_out may not alias an input) */
+int zk_dev_mle_tensor(zk_ctx* ctx, zk_field field, zk_mle_op op, const void* d_a, uint64_t na, const void* d_b,
+                      uint64_t nb, void* d_out);
 /* gkr_prove over device tables (read-only; the ctx workspace holds the folds) */
 int zk_dev_gkr_sumcheck_prove(zk_ctx* ctx, zk_field field, const void* const d_tables[4], uint32_t nvars,
                               zk_repr repr, const zk_fe* claimed_sum, zk_transcript* transcript,

@@ -177,6 +177,15 @@ def evaluate(p: int, evals: list[int], point: list[int]) -> int:  # :79-91
     return cur[0]
 
 
+def scale(p: int, a: list[int], v: int) -> list[int]:  # :93-97
+    return [x * v % p for x in a]
+
+
+def binop(p: int, a: list[int], b: list[int], op: str) -> list[int]:  # impl Add/Mul/Sub :113-151 (zip)
+    f = {"add": lambda x, y: x + y, "mul": lambda x, y: x * y, "sub": lambda x, y: x - y}[op]
+    return [f(x, y) % p for x, y in zip(a, b)]
+
+
 def tensor_add_mul(p: int, a: list[int], b: list[int], op: str) -> list[int]:  # :99-110
     if op == "add":
         return [(x + y) % p for x in a for y in b]

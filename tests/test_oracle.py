@@ -189,3 +189,11 @@ def test_golden_gkr_ref_2var(golden, fast):
     polys, chal = co.gkr_prove(g["field"], [co.to_limbs(t) for t in g["tables"]], co.Transcript(), fast=fast)
     assert polys == [[h2i(c) for c in p] for p in g["round_polys"]]
     assert chal == [h2i(c) for c in g["challenges"]]
+
+
+def test_oracle_scale_and_binop():  # multilinear_polynomial_evaluation.rs:93-97, :113-151 (zip)
+    p = po.MODULI[0]
+    assert po.scale(p, [0, 1, p - 1], 3) == [0, 3, p - 3]
+    assert po.binop(p, [1, 2, 3, 4], [5, 6], "add") == [6, 8]
+    assert po.binop(p, [1, 2], [5, 6, 7, 8], "sub") == [p - 4, p - 4]
+    assert po.binop(p, [2, 3], [4, 5], "mul") == [8, 15]

@@ -1245,6 +1245,40 @@ __global__ __launch_bounds__(kBlock) void k_fold4(const Fe* __restrict__ A, cons
 }
 
 // ---------------------------------------------------------------------------
+// The table builders on either side of the sum-check (multilinear_polynomial_
+// evaluation.rs): element-wise Add / Mul / Sub of two MLEs (:113-151, zip ->
+// the shorter length), scale (:93-97: op MUL against the broadcast scalar) and
+// tensor_add_mul_polynomials (:99-110: out[i nb + j] = op(a[i], b[j]), which is
+// how a GKR layer's S = w_b + w_c and P = w_b * w_c are laid out). Streaming:
+// one 32-B store per output, the tensor's operands are L2-resident re-reads.
+// ---------------------------------------------------------------------------
+enum MleOp : uint32_t { MLE_ADD = 0, MLE_MUL = 1, MLE_SUB = 2 };
+
+template <class F>
+__device__ __forceinline__ Fe mle_apply(uint32_t op, const Fe& a, const Fe& b) {
+  return op == MLE_ADD ? fe_add<F>(a, b) : op == MLE_MUL ? fe_mul<F>(a, b) : fe_sub<F>(a, b);
+}
+
+// Y[i] = op(X[i], Z ? Z[i] : s)
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_mle_map(const Fe* __restrict__ X, const Fe* __restrict__ Z, Fe s,
+                                                    Fe* __restrict__ Y, uint64_t n, uint32_t op) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    st_fe(Y, i, mle_apply<F>(op, ld_fe(X, i), Z ? ld_fe(Z, i) : s));
+}
+
+// Y[i << lgb | j] = op(A[i], B[j]) over na << lgb outputs
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_mle_tensor(const Fe* __restrict__ A, const Fe* __restrict__ B,
+                                                       Fe* __restrict__ Y, uint64_t n, uint32_t lgb, uint32_t op) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t bm = ((uint64_t)1 << lgb) - 1;
+  for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < n; t += stride)
+    st_fe(Y, t, mle_apply<F>(op, ld_fe(A, t >> lgb), ld_fe(B, t & bm)));
+}
+
+// ---------------------------------------------------------------------------
 // canonical <-> Montgomery (in place allowed)
 // ---------------------------------------------------------------------------
 template <class F, bool TO_MONT>

@@ -177,6 +177,82 @@ int zk_mle_partial_evaluate(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe
   });
 }
 
+// impl Add / Mul / Sub for MultilinearPoly (:113-151): zip -> the shorter table
+int zk_mle_binop(zk_ctx* c, zk_field field, zk_repr repr, zk_mle_op op, const zk_fe* a, uint32_t nvars_a,
+                 const zk_fe* b, uint32_t nvars_b, zk_fe* out) {
+  return guarded([&] {
+    require(c && a && b && out, "null argument");
+    require(op == ZK_MLE_ADD || op == ZK_MLE_MUL || op == ZK_MLE_SUB, "unknown op");
+    require(pow2_ok(nvars_a) && pow2_ok(nvars_b), "table too large");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t na = (uint64_t)1 << nvars_a, nb = (uint64_t)1 << nvars_b, n = std::min(na, nb);
+      c->input.ensure(2 * n * 32);
+      c->work[0].ensure(n * 32);
+      upload<F>(c, repr, a, n, c->input.fe());
+      upload<F>(c, repr, b, n, c->input.fe() + n);
+      const uint32_t grid = grid_for(c, n, zk::k_mle_map<F>);
+      launch(c, ZK_K_CONVERT, 96.0 * n, op == ZK_MLE_MUL ? (double)n : 0.0, zk::k_mle_map<F>, grid,
+             c->input.fe(), c->input.fe() + n, Fe{}, c->work[0].fe(), n, (uint32_t)op);
+      download<F>(c, repr, c->work[0].fe(), n, out);
+    });
+  });
+}
+
+// scale(value) (:93-97)
+int zk_mle_scale(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars, const zk_fe* value,
+                 zk_fe* out) {
+  return guarded([&] {
+    require(c && evals && value && out, "null argument");
+    require(pow2_ok(nvars), "table too large");
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t n = (uint64_t)1 << nvars;
+      const Fe s = in_mont<F>(repr, *value);
+      c->input.ensure(n * 32);
+      c->work[0].ensure(n * 32);
+      upload<F>(c, repr, evals, n, c->input.fe());
+      const uint32_t grid = grid_for(c, n, zk::k_mle_map<F>);
+      launch(c, ZK_K_CONVERT, 64.0 * n, (double)n, zk::k_mle_map<F>, grid, c->input.fe(), (const Fe*)nullptr, s,
+             c->work[0].fe(), n, (uint32_t)zk::MLE_MUL);
+      download<F>(c, repr, c->work[0].fe(), n, out);
+    });
+  });
+}
+
+// tensor_add_mul_polynomials (:99-110); MultilinearPoly::new panics unless the
+// product length is a power of two (so both lengths are)
+static void check_tensor(zk_mle_op op, uint64_t na, uint64_t nb) {
+  require(op == ZK_MLE_ADD || op == ZK_MLE_MUL, "tensor op must be Add or Mul (Operation)");
+  require(na >= 1 && nb >= 1, "Invalid evaluations (empty tensor)");
+  require((na & (na - 1)) == 0 && (nb & (nb - 1)) == 0, "Invalid evaluations (length not a power of two)");
+  require(na <= ((uint64_t)1 << 39) / nb, "table too large");
+}
+
+int zk_mle_tensor(zk_ctx* c, zk_field field, zk_repr repr, zk_mle_op op, const zk_fe* a, uint64_t na,
+                  const zk_fe* b, uint64_t nb, zk_fe* out) {
+  return guarded([&] {
+    require(c && a && b && out, "null argument");
+    check_tensor(op, na, nb);
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t n = na * nb;
+      c->input.ensure((na + nb) * 32);
+      c->work[0].ensure(n * 32);
+      upload<F>(c, repr, a, na, c->input.fe());
+      upload<F>(c, repr, b, nb, c->input.fe() + na);
+      const uint32_t lgb = (uint32_t)__builtin_ctzll(nb);
+      const uint32_t grid = grid_for(c, n, zk::k_mle_tensor<F>);
+      launch(c, ZK_K_CONVERT, 32.0 * n, op == ZK_MLE_MUL ? (double)n : 0.0, zk::k_mle_tensor<F>, grid,
+             c->input.fe(), c->input.fe() + na, c->work[0].fe(), n, lgb, (uint32_t)op);
+      download<F>(c, repr, c->work[0].fe(), n, out);
+    });
+  });
+}
+
 int zk_mle_evaluate(zk_ctx* c, zk_field field, zk_repr repr, const zk_fe* evals, uint32_t nvars,
                     const zk_fe* point, uint32_t npoint, zk_fe* out) {
   return guarded([&] {
@@ -411,6 +487,25 @@ int zk_dev_mle_partial_evaluate(zk_ctx* c, zk_field field, const void* d_in, uin
       const uint32_t grid = grid_for(c, half, zk::k_fold<F>);
       const uint32_t s = nvars - 1 - bit;
       launch(c, ZK_K_FOLD, 96.0 * half, (double)half, zk::k_fold<F>, grid, reinterpret_cast<const Fe*>(d_in), reinterpret_cast<Fe*>(d_out), half, s, r);
+      sync(c);
+    });
+  });
+}
+int zk_dev_mle_tensor(zk_ctx* c, zk_field field, zk_mle_op op, const void* d_a, uint64_t na, const void* d_b,
+                      uint64_t nb, void* d_out) {
+  return guarded([&] {
+    require(c && d_a && d_b && d_out, "null argument");
+    require(d_out != d_a && d_out != d_b, "d_out may not alias an input");
+    check_tensor(op, na, nb);
+    bind(c);
+    dispatch(field, [&](auto f) {
+      using F = decltype(f);
+      const uint64_t n = na * nb;
+      const uint32_t lgb = (uint32_t)__builtin_ctzll(nb);
+      const uint32_t grid = grid_for(c, n, zk::k_mle_tensor<F>);
+      launch(c, ZK_K_CONVERT, 32.0 * n, op == ZK_MLE_MUL ? (double)n : 0.0, zk::k_mle_tensor<F>, grid,
+             reinterpret_cast<const Fe*>(d_a), reinterpret_cast<const Fe*>(d_b), reinterpret_cast<Fe*>(d_out), n,
+             lgb, (uint32_t)op);
       sync(c);
     });
   });

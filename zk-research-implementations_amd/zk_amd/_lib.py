@@ -60,6 +60,9 @@ SIGNATURES = {
     "zk_fe_vec_to_bytes": (I, [I, I, P, SZ, P]),
     "zk_mle_partial_evaluate": (I, [P, I, I, P, U32, U32, P, P]),
     "zk_mle_evaluate": (I, [P, I, I, P, U32, P, U32, P]),
+    "zk_mle_binop": (I, [P, I, I, I, P, U32, P, U32, P]),
+    "zk_mle_scale": (I, [P, I, I, P, U32, P, P]),
+    "zk_mle_tensor": (I, [P, I, I, I, P, U64, P, U64, P]),
     "zk_sumcheck_prove": (I, [P, I, I, P, U32, P, P]),
     "zk_sumcheck_verify": (I, [P, I, I, P, U32, P, U32, U32, P, C.POINTER(C.c_int)]),
     "zk_gkr_sumcheck_prove": (I, [P, I, I, P, U32, P, P, P, P, P, P]),
@@ -92,6 +95,7 @@ SIGNATURES = {
     "zk_dev_download": (I, [P, I, I, P, SZ, P]),
     "zk_dev_synth_fill": (I, [P, I, P, U64, U64, U32, U64, U64]),
     "zk_dev_mle_partial_evaluate": (I, [P, I, P, U32, U32, I, P, P]),
+    "zk_dev_mle_tensor": (I, [P, I, I, P, U64, P, U64, P]),
     "zk_dev_gkr_sumcheck_prove": (I, [P, I, P, U32, I, P, P, P, P, P]),
     "zk_ctx_attach_host_comm": (I, [P, I, I, ALLREDUCE_FN, P]),
     "zk_comm_get_unique_id": (I, [P]),

@@ -24,6 +24,8 @@ from ._lib import ZK_BLOB_GKR, ZK_BLOB_SUMCHECK, ZK_EINVAL, ZkError, check, lib
 from .context import REPR_CANONICAL, Context
 from .elems import as_limbs, one, ptr, to_ints
 
+MLE_ADD, MLE_MUL, MLE_SUB = 0, 1, 2  # zk_mle_op
+
 
 class Field(IntEnum):
     BN254_FR = 0
@@ -154,6 +156,40 @@ class MultilinearPoly:
         )
         return to_ints(out)[0]
 
+    def scale(self, value: int) -> "MultilinearPoly":  # :93-97
+        out = np.zeros_like(self.limbs)
+        _call(lib().zk_mle_scale(self._ctx().h, int(self.field), REPR_CANONICAL, ptr(self.limbs), self.num_of_vars,
+                                 ptr(one(value)), ptr(out)))
+        return MultilinearPoly(out, self.field, self.ctx)
+
+    def _binop(self, other: "MultilinearPoly", op: int) -> "MultilinearPoly":  # impl Add/Mul/Sub :113-151
+        if not isinstance(other, MultilinearPoly):
+            return NotImplemented
+        out = np.zeros((min(self.limbs.shape[0], other.limbs.shape[0]), 4), np.uint64)
+        _call(lib().zk_mle_binop(self._ctx().h, int(self.field), REPR_CANONICAL, op, ptr(self.limbs),
+                                 self.num_of_vars, ptr(other.limbs), other.num_of_vars, ptr(out)))
+        return MultilinearPoly(out, self.field, self.ctx)
+
+    def __add__(self, other):
+        return self._binop(other, MLE_ADD)
+
+    def __mul__(self, other):
+        return self._binop(other, MLE_MUL)
+
+    def __sub__(self, other):
+        return self._binop(other, MLE_SUB)
+
+    @staticmethod
+    def tensor_add_mul_polynomials(poly_a, poly_b, op, field: int = Field.BN254_FR,
+                                   ctx: Context | None = None) -> "MultilinearPoly":  # :99-110
+        """op: gkr.Operation (Add = 0, Mul = 1) or the strings "add" / "mul"."""
+        code = {"add": MLE_ADD, "mul": MLE_MUL}[op] if isinstance(op, str) else int(op)
+        a, b = as_limbs(poly_a), as_limbs(poly_b)
+        out = np.zeros((a.shape[0] * b.shape[0], 4), np.uint64)
+        _call(lib().zk_mle_tensor((ctx or default_context()).h, int(field), REPR_CANONICAL, code, ptr(a),
+                                  a.shape[0], ptr(b), b.shape[0], ptr(out)))
+        return MultilinearPoly(out, field, ctx)
+
     def __eq__(self, other) -> bool:
         return (
             isinstance(other, MultilinearPoly)
@@ -182,6 +218,9 @@ class ProductPoly:
             acc = acc * poly.evaluate(values) % p
         return acc
 
+    def reduce(self) -> list[int]:  # :52-54: evaluation[0] * evaluation[1]
+        return (self.evaluation[0] * self.evaluation[1]).evaluation
+
     def partial_evaluate(self, value: int) -> "ProductPoly":  # :38-50
         return ProductPoly([poly.partial_evaluate(0, value).limbs for poly in self.evaluation], self.field,
                            self.evaluation[0].ctx)
@@ -206,6 +245,10 @@ class SumPoly:
 
     def partial_evaluate(self, value: int) -> "SumPoly":  # :78-86
         return SumPoly([pp.partial_evaluate(value) for pp in self.polys])
+
+    def reduce(self) -> list[int]:  # :88-99: polys[0].reduce() + polys[1].reduce() (zip)
+        p = modulus(self.field)
+        return [(x + y) % p for x, y in zip(self.polys[0].reduce(), self.polys[1].reduce())]
 
     def gkr_tables(self) -> list[np.ndarray]:
         """The four tables SumPoly::reduce reads (:88-99 with :52-54):
