@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-config5", action="store_true", help="skip BLS12-381 GKR + KZG commit (BASELINE config 5)")
     ap.add_argument("--no-config4", dest="config4", action="store_false",
                     help="skip the 26-variable-total proof split over all ranks (BASELINE config 4, strong scaling)")
+    ap.add_argument("--force-rccl", action="store_true",
+                    help="diagnostic: at world 1 route every step through ncclAllReduce (the multi-rank data path)")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
     return ap.parse_args()
 
@@ -332,6 +334,12 @@ def config4_bench(ctx, field: int, world: int, rank: int, barrier, total_nvars: 
 
 def main() -> None:
     args = parse()
+    # stdout carries exactly ONE line, the JSON result: libraries that print
+    # banners to stdout (RCCL's "RCCL version ..." at communicator init) are
+    # sent to stderr by pointing fd 1 there; the result goes to the saved fd.
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -352,7 +360,11 @@ def main() -> None:
     from zk_amd.elems import as_limbs, ptr
 
     torch.cuda.set_device(local)
+    if args.force_rccl and world == 1:
+        os.environ["ZK_FORCE_COLLECTIVES"] = "1"  # read at zk_ctx_create
     ctx = zk_amd.Context(local)
+    if args.force_rccl and world == 1:
+        ctx.attach_rccl(0, 1, rccl_unique_id())
     lg = (world - 1).bit_length()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -515,7 +527,7 @@ def main() -> None:
             cb = cpu_baseline(field, args.cpu_sample_nvars, args.cpu_fast_nvars)
             out["cpu_baseline"] = cb
             out["speedup_vs_cpu_baseline"] = value / cb["value"]
-        print(json.dumps(out), flush=True)
+        os.write(result_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
