@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--no-config5", action="store_true", help="skip BLS12-381 GKR + KZG commit (BASELINE config 5)")
     ap.add_argument("--no-config4", dest="config4", action="store_false",
                     help="skip the 26-variable-total proof split over all ranks (BASELINE config 4, strong scaling)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="N>1 data path: RCCL (default) or, as a diagnostic that rehearses the multi-rank bench "
+                    "on one card, a gloo host all-reduce with every rank on device LOCAL_RANK %% device_count")
     ap.add_argument("--force-rccl", action="store_true",
                     help="diagnostic: at world 1 route every step through ncclAllReduce (the multi-rank data path)")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
@@ -359,6 +362,8 @@ def main() -> None:
     from zk_amd.context import rccl_unique_id
     from zk_amd.elems import as_limbs, ptr
 
+    if args.comm == "host":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if args.force_rccl and world == 1:
         os.environ["ZK_FORCE_COLLECTIVES"] = "1"  # read at zk_ctx_create
@@ -369,9 +374,14 @@ def main() -> None:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
-        obj = [rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.attach_rccl(rank, world, obj[0])
+        if args.comm == "host":
+            from zk_amd.dist import TorchAllreduce
+
+            ctx.attach_host_comm(rank, world, TorchAllreduce())
+        else:
+            obj = [rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.attach_rccl(rank, world, obj[0])
 
     nloc = args.nvars
     n = nloc + lg
@@ -481,7 +491,8 @@ def main() -> None:
                 "nvars_total": n,
                 "nvars_per_gpu": nloc,
                 "parallelism": f"hypercube split over {world} GPU(s) by low index bits; "
-                "1 RCCL all-reduce (24 x u64) per round" if world > 1 else "single GPU",
+                + ("1 RCCL all-reduce (24 x u64) per round" if args.comm == "rccl" else
+                   "host (gloo) all-reduce per round: diagnostic, not the product path") if world > 1 else "single GPU",
             },
             "roofline": {
                 "bound": "hbm",
