@@ -416,7 +416,7 @@ def main() -> None:
             # during the LAST timed step only: their marker packets cost the GPU
             # ~5 us per round, so timing every step would inflate ms_per_step
             st0 = ctx.stats()
-            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail"])
+            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0"])
         step()
     torch.cuda.synchronize()
     barrier()
@@ -440,8 +440,8 @@ def main() -> None:
         d["ms"] = k[name]["ms"]
         return d
 
-    rnd = kind("gkr_round")
     round_kinds = {
+        "gkr_d0": "k_gkr_d0r (rounds 0 and 1 in one pass over the input tables: nine grid-point product sums, nothing written)",
         "gkr_round0": "k_gkr_round0 (round 0: e0, e1, e2 over the input tables)",
         "gkr_round": "k_gkr_round (round 1: fold by r0 + round sums)",
         "gkr_round_lanes": "k_gkr_round_lanes (single small rounds, 8 lanes per pair)",
@@ -456,6 +456,10 @@ def main() -> None:
             per_kind[name] = {"kernel": desc, "launches": d["launches"], "ms": d["ms"],
                               "alg_GB": d["alg_bytes"] / 1e9,
                               "achieved_GBs": d["alg_bytes"] / (d["ms"] / 1e3) / 1e9 if d["ms"] else None}
+    # the dominant kernel: the kind with the longest average launch (k_gkr_d0r with
+    # ZK_D0 on, k_gkr_round — round 1 — with it off)
+    dom = max(per_kind, key=lambda nm: per_kind[nm]["ms"] / per_kind[nm]["launches"])
+    rnd = kind(dom)
     all_b = sum(kind(nm)["alg_bytes"] for nm in per_kind)
     all_ms = sum(kind(nm)["ms"] for nm in per_kind)
     achieved = rnd["alg_bytes"] / (rnd["ms"] / 1e3) / 1e9 if rnd["ms"] else 0.0
@@ -466,7 +470,7 @@ def main() -> None:
     tpath = os.path.join(ROOT, "profiles", "r1_traffic.json")
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
-        if t.get("kernel") == "k_gkr_round" and field == 0:  # per-symbol summary of this workload
+        if t.get("kind") == dom and field == 0:  # per-symbol summary of this workload
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
             traffic_src = f"profiles/r1_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
@@ -496,7 +500,10 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_gkr_round (round 1: fused fold by r0 + round evaluation; the longest launch)",
+                "kernel": round_kinds[dom] + "; the longest launch",
+                "bound_note": "k_gkr_d0r is VALU-bound (multiply issue: nine unreduced 256-bit products per "
+                "quad and table pair), so its HBM fraction is below round 1's; the proof is faster with it "
+                "(DESIGN.md section 3)" if dom == "gkr_d0" else None,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -299,15 +299,16 @@ def test_stats_and_timing(ctx):
     ctx.set_timing(False)
     st = ctx.stats()
     k = st["kernels"]
-    # round 0, round 1 alone, then rounds (2,3) .. (10,11) two per step; these
-    # small double steps run in one persistent kernel (k_gkr_dtail)
-    assert k["gkr_round0"]["launches"] == 1 and k["gkr_dtail"]["launches"] == 1 and k["gkr_dround"]["launches"] == 0
-    assert k["gkr_round"]["launches"] + k["gkr_round_lanes"]["launches"] == 1
-    # first double: 1 pending challenge (level 1 -> 2), then 2 pending
+    # rounds 0 and 1 in one pass over the inputs (k_gkr_d0r, ZK_D0 default), then
+    # rounds (2,3) .. (10,11) two per step, each folding by two pending challenges
+    # (the first straight from the inputs); these small steps run in one persistent
+    # kernel (k_gkr_dtail)
+    assert k["gkr_d0"]["launches"] == 1 and k["gkr_dtail"]["launches"] == 1 and k["gkr_dround"]["launches"] == 0
+    assert k["gkr_round0"]["launches"] + k["gkr_round"]["launches"] + k["gkr_round_lanes"]["launches"] == 0
     q = [1 << (n - 4 - 2 * d) for d in range((n - 2) // 2)]  # quads of each double step (Z = 4Q)
-    assert k["gkr_dtail"]["alg_bytes"] == 1536 * q[0] + 2560 * sum(q[1:])
-    assert k["gkr_dtail"]["ms"] > 0 and st["host_syncs"] >= 2 + (n - 2) // 2
-    assert k["gkr_round0"]["alg_bytes"] == 256 * (1 << (n - 1))
+    assert k["gkr_dtail"]["alg_bytes"] == 2560 * sum(q)
+    assert k["gkr_dtail"]["ms"] > 0 and st["host_syncs"] >= 1 + (n - 2) // 2
+    assert k["gkr_d0"]["alg_bytes"] == 128 * (1 << n)
 
 
 @pytest.mark.parametrize("field", FIELDS)

@@ -5,9 +5,9 @@
   each round after its challenge), and equal to the oracle's.
 * From round 2 on two rounds run per kernel (k_gkr_dround, default); the
   proof is identical with one round per kernel (ZK_DROUND=0), for odd and
-  even round counts, pre-enqueued or not. With ZK_D0=1 (off by default:
-  measured slower) even counts run rounds 0 and 1 in one pass over the
-  inputs (k_gkr_d0); the proof is identical.
+  even round counts, pre-enqueued or not. With ZK_D0=1 (default) even counts
+  run rounds 0 and 1 in one pass over the inputs (k_gkr_d0r; ZK_D0=2 the
+  8-lane k_gkr_d0); the proof is identical to ZK_D0=0 (round 0, then round 1).
 * The small double steps run in one persistent kernel (k_gkr_dtail, default);
   the proof is identical with one launch per step (ZK_DTAIL=0), when it
   starts at the first double step over large tables (ZK_DTAIL_MAX_QUADS) and
@@ -124,11 +124,11 @@ def test_double_and_single_rounds_agree_20var(monkeypatch, field):
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_first_double_step_matches_oracle(monkeypatch, field, n):
     """With ZK_D0=1 even variable counts start with rounds 0 and 1 in one pass
-    over the inputs (k_gkr_d0: nine product sums, nothing written); ZK_D0=0
+    over the inputs (k_gkr_d0r: nine product sums, nothing written); ZK_D0=0
     runs round 0 alone and round 1 as a single step. Both equal the oracle, pre-enqueued
     and per-round launched."""
     want = _oracle(field, n)
-    for d0 in ("1", "0"):
+    for d0 in ("1", "2", "0"):  # 1: k_gkr_d0r (3 lanes per quad-product, default), 2: k_gkr_d0 (8 lanes)
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_D0", d0)
             monkeypatch.setenv("ZK_PRELAUNCH", pre)
@@ -143,14 +143,14 @@ def test_first_double_step_matches_oracle(monkeypatch, field, n):
 def test_first_double_step_agrees_22var(monkeypatch, field):
     n = 22
     got = {}
-    for d0 in ("1", "0"):
+    for d0 in ("1", "2", "0"):
         monkeypatch.setenv("ZK_D0", d0)
         ctx = zk_amd.Context(0)
         try:
             got[d0] = _prove(ctx, field, n)
         finally:
             ctx.close()
-    assert got["1"] == got["0"]
+    assert got["1"] == got["0"] == got["2"]
 
 
 @pytest.mark.parametrize("field", [0, 2])

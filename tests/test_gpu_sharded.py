@@ -59,11 +59,11 @@ def _oracle(field: int, n: int) -> dict:
             "blob_keccak": po.keccak256(po.proof_blob(po.BLOB_GKR, field, 0, [list(p) for p in polys])).hex()}
 
 
-def _steps(nloc: int, d0: bool = False) -> int:
+def _steps(nloc: int, d0: bool = True) -> int:
     """Kernel steps of a phase of nloc rounds, one all-reduce each: round 0,
     round 1, one more single round if nloc - 2 is odd, then two rounds per step.
-    With ZK_D0=1 an even phase runs rounds 0 and 1 in one step."""
-    if d0 and nloc % 2 == 0:
+    With ZK_D0 (default) an even phase runs rounds 0 and 1 in one step."""
+    if d0 and nloc >= 2 and nloc % 2 == 0:
         return nloc // 2
     if nloc <= 2:
         return nloc

@@ -28,17 +28,23 @@ def dispatches(path, counter):
     return [out[k] for k in sorted(out)]
 
 
-def schedule(n, dtail_max_quads=4096):
-    """(symbol prefix, algorithmic bytes) per dispatch of one proof (pre-enqueued, one GPU)."""
-    st = [("zk::k_gkr_round0", 256.0 * (1 << (n - 1)))]
-    if n >= 2:
-        st.append(("zk::k_gkr_round", 768.0 * (1 << (n - 2))))
-    i = 2
-    if n >= 3 and (n - 2) % 2 == 1:
-        st.append(("zk::k_gkr_round", 768.0 * (1 << (n - 3))))
-        i = 3
+def schedule(n, dtail_max_quads=4096, d0=True):
+    """(symbol prefix, algorithmic bytes) per dispatch of one proof (pre-enqueued, one GPU).
+    d0 (ZK_D0, default): an even n starts with k_gkr_d0r (rounds 0 and 1, 128 B per
+    input index) and every double step then folds by two pending challenges."""
+    if d0 and n >= 2 and n % 2 == 0:
+        st = [("zk::k_gkr_d0r", 128.0 * (1 << n))]
+        i, np_ = 2, 2
+    else:
+        st = [("zk::k_gkr_round0", 256.0 * (1 << (n - 1)))]
+        if n >= 2:
+            st.append(("zk::k_gkr_round", 768.0 * (1 << (n - 2))))
+        i = 2
+        if n >= 3 and (n - 2) % 2 == 1:
+            st.append(("zk::k_gkr_round", 768.0 * (1 << (n - 3))))
+            i = 3
+        np_ = 1
     doubles = []
-    np_ = 1
     while i + 1 < n:
         q = (1 << (n - i)) // 4
         doubles.append((q, np_))
@@ -61,8 +67,10 @@ def main():
     write = dispatches(f"{root}/gpurun_out/prof_{tag}_write/run_counter_collection.csv", "WRITE_SIZE")
     sched = schedule(nvars, dmax)
 
+    first = sched[0][0]
+
     def last_proof(ds):
-        start = max(k for k, d in enumerate(ds) if "k_gkr_round0" in d[0])
+        start = max(k for k, d in enumerate(ds) if d[0].startswith(first))
         return [d for d in ds[start:] if "k_gkr_" in d[0]][: len(sched)]
 
     f, w = last_proof(fetch), last_proof(write)
@@ -79,9 +87,13 @@ def main():
         return {"launches": len(rs), "traffic_bytes_per_launch": t / max(1, len(rs)),
                 "alg_bytes_per_launch": a / max(1, len(rs)), "traffic_over_alg": t / a if a else None}
 
-    big = summary(lambda k: k.startswith("zk::k_gkr_round<"))
-    res = {"kernel": "k_gkr_round", "nvars": nvars, **big,
+    if first == "zk::k_gkr_d0r":  # the longest launch of the proof (bench.py's dominant kernel)
+        big, name, kind = summary(lambda k: k.startswith(first)), "k_gkr_d0r", "gkr_d0"
+    else:
+        big, name, kind = summary(lambda k: k.startswith("zk::k_gkr_round<")), "k_gkr_round", "gkr_round"
+    res = {"kernel": name, "kind": kind, "nvars": nvars, **big,
            "others": {"k_gkr_round0": summary(lambda k: "k_gkr_round0" in k),
+                      "k_gkr_round": summary(lambda k: k.startswith("zk::k_gkr_round<")),
                       "k_gkr_dround": summary(lambda k: "k_gkr_dround" in k),
                       "k_gkr_dtail": summary(lambda k: "k_gkr_dtail" in k)},
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "

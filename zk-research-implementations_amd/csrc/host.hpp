@@ -202,7 +202,7 @@ struct zk_ctx {
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
-  bool d0 = false;          // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0=1; measured slower)
+  int d0 = 1;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel: 1 k_gkr_d0r, 2 k_gkr_d0, 0 off (ZK_D0)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
@@ -597,8 +597,14 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     if (st.kind == GS_D0) {  // rounds 0 and 1 over the input tables (size 4Q), nothing written
       const uint64_t Q = size / 4;
-      const uint32_t grid = grid_for(c, zk::kDQuads * Q, zk::k_gkr_d0<F>);
-      launch(c, ZK_K_GKR_ROUND0, 128.0 * size, 4.5 * size, zk::k_gkr_d0<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
+      if (c->d0 == 2) {  // ZK_D0=2: the 8-lane k_gkr_d0 (DPP exchange, V11 in schoolbook rows)
+        const uint32_t grid = grid_for(c, zk::kDQuads * Q, zk::k_gkr_d0<F>);
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
+      } else {  // a quad-product per three lanes, one grid row each (k_gkr_d0r)
+        const uint64_t threads = (2 * Q + zk::kD0RUnits - 1) / zk::kD0RUnits * 64;
+        const uint32_t grid = grid_for(c, threads, zk::k_gkr_d0r<F>);
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0r<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
+      }
       enqueue_reduce(c, sk, across_ranks, zk::kD0Limbs);
       return;
     }

@@ -1072,6 +1072,95 @@ __global__ __launch_bounds__(kBlock) void k_gkr_d0(const Fe* __restrict__ A, con
   grid_finish<kD0Limbs>(sc, sink);
 }
 
+// Extended grid point 2 hi - lo. For fields with 3p < 2^256 (BN254) it is lazy,
+// 2 hi + (p - lo) in [0, 3p): product sums of such operands stay exact
+// integers congruent mod p (the consumer reduces 17-word totals of any size,
+// hlimbs_to_fe). lo must be reduced.
+template <class F>
+constexpr bool kLazyExt = (uint64_t)F::P[7] * 3 + 3 < (1ull << 32);
+template <class F>
+__device__ __forceinline__ Fe ext2(const Fe& lo, const Fe& hi) {  // 2 hi - lo (mod p), lo < p
+  if constexpr (kLazyExt<F>) {
+    Fe d, r;
+    uint32_t b = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d.v[i] = subb32(F::P[i], lo.v[i], b, &b);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = addc32(hi.v[i], hi.v[i], c, &c);
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = addc32(r.v[i], d.v[i], c, &c);
+    return r;
+  } else {
+    return at2<F>(lo, hi);
+  }
+}
+// ---------------------------------------------------------------------------
+// k_gkr_d0r: a quad-product per THREE lanes, lane a forming grid row a
+// (points (a,0), (a,1), (a,2)): rows 0 and 1 start from the corners, row 2
+// from V(2,b) = 2 V(1,b) - V(0,b) (reduced), and V(a,2) = ext2(V(a,0), V(a,1)).
+// Nine products over nine slots (no empty slot), three accumulators per lane
+// (fewer VGPRs, more waves per SIMD); 21 units per wave, lane 63 idle.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kD0RUnits = 21;                // units per wave
+constexpr uint32_t kD0RQuads = 2 * kD0RUnits;     // quads per block iteration (2 waves per product)
+template <class F>
+__global__ __launch_bounds__(kBlock, 2) void k_gkr_d0r(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                      const Fe* __restrict__ M, const Fe* __restrict__ P,
+                                                      uint64_t Q, RoundSink sink) {
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  __shared__ DScratch sc;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t unit = (lane * 43u) >> 7, a = lane - 3 * unit;  // lane / 3, lane % 3 for lane < 64
+  const uint32_t pp = wv & 1, jl = (wv >> 1) * kD0RUnits + unit;
+  const Fe* __restrict__ X = pp ? M : A;
+  const Fe* __restrict__ Z = pp ? P : S;
+  Wide acc[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) acc[s] = wide_zero<F>();
+  if (unit < kD0RUnits) {
+    for (uint64_t jb = (uint64_t)blockIdx.x * kD0RQuads; jb < Q; jb += (uint64_t)gridDim.x * kD0RQuads) {
+      const uint64_t j = jb + jl;
+      if (j < Q) {  // uniform over the 3 lanes of a unit
+        const Fe x00 = ld_fe(X, j), x01 = ld_fe(X, j + Q), x10 = ld_fe(X, j + 2 * Q), x11 = ld_fe(X, j + 3 * Q);
+        const Fe z00 = ld_fe(Z, j), z01 = ld_fe(Z, j + Q), z10 = ld_fe(Z, j + 2 * Q), z11 = ld_fe(Z, j + 3 * Q);
+        __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
+        const Fe x0 = a == 2 ? at2<F>(x00, x10) : sel_fe(a == 0, x00, x10);
+        const Fe z0 = a == 2 ? at2<F>(z00, z10) : sel_fe(a == 0, z00, z10);
+        wide_mac<F>(acc[0], x0, z0);
+        const Fe x1 = a == 2 ? at2<F>(x01, x11) : sel_fe(a == 0, x01, x11);
+        const Fe z1 = a == 2 ? at2<F>(z01, z11) : sel_fe(a == 0, z01, z11);
+        wide_mac<F>(acc[1], x1, z1);
+        wide_mac<F>(acc[2], ext2<F>(x0, x1), ext2<F>(z0, z1));
+      }
+    }
+  }
+  // block limb sums, one slot (column b of the grid) at a time; category of point (a, b):
+  // 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21, 7 V12, 8 V11 (host.hpp two_rounds)
+  constexpr int kCat[3][3] = {{0, 2, 3}, {4, 8, 7}, {5, 6, 1}};
+  const uint32_t t = threadIdx.x;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+#pragma unroll
+    for (int w = 0; w < 17; ++w) sc.rows[t * 17 + w] = acc[b].w[w];
+    __syncthreads();
+    if (t < 204) {  // wave part (t / 51) sums its 21 lanes of row ra
+      const uint32_t part = t / 51, r = t % 51, ra = r / 17, w = r % 17;
+      uint64_t s0 = 0;
+#pragma unroll 7
+      for (uint32_t u = 0; u < kD0RUnits; ++u) s0 += sc.rows[(part * 64 + 3 * u + ra) * 17 + w];
+      sc.pp[t] = s0;
+    }
+    __syncthreads();
+    if (t < 51) {
+      const uint32_t ra = t / 17, w = t % 17;
+      sc.tot[kCat[ra][b] * 17 + w] = sc.pp[t] + sc.pp[51 + t] + sc.pp[102 + t] + sc.pp[153 + t];
+    }
+    __syncthreads();
+  }
+  grid_finish<kD0Limbs>(sc, sink);
+}
+
 // ---------------------------------------------------------------------------
 // The small double rounds of a proof in ONE persistent kernel: step s is the
 // k_gkr_dround step over Q0 >> 2s quads (two pending challenges, the first
