@@ -202,7 +202,7 @@ struct zk_ctx {
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
-  int d0 = -1;             // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 1 k_gkr_d0r, 2 k_gkr_d0, 0 off, -1 (unset) k_gkr_d0r where its extended points are lazy (BN254)
+  int d0 = 1;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
@@ -525,11 +525,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   const uint64_t L = (uint64_t)1 << nv;
   const bool pre = prelaunch(c, nv);
   std::vector<GStep> steps;
-  // rounds 0 and 1 in one pass over the inputs; by default only where k_gkr_d0r's
-  // extended points are lazy (BN254: 1.70 vs 1.78 ms at n = 24; BLS12-381 Fr
-  // measured slower with fully reduced ones)
-  const bool d0_on = c->d0 > 0 || (c->d0 < 0 && zk::kLazyExt<F>);
-  const bool d0 = c->dround && d0_on && nv >= 2 && nv % 2 == 0;
+  // rounds 0 and 1 in one pass over the inputs (default; same-box A/B at n = 24:
+  // BN254 Fr 1.72-1.74 vs 1.82-1.85 ms, BLS12-381 Fr 1.76 vs 1.83 ms)
+  const bool d0 = c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
   if (nv >= 1) steps.push_back({d0 ? GS_D0 : GS_ROUND0, 0, 0});
   if (c->dround) {
     uint32_t i = d0 ? 2 : 1;
