@@ -363,14 +363,9 @@ def main() -> None:
     from zk_amd.elems import as_limbs, ptr
 
     if args.comm == "host":
-        ndev = torch.cuda.device_count()
-        if world > ndev:
-            # Ranks share a card (one-card rehearsal): a pre-enqueued step of one
-            # rank spins on its challenge while holding the CUs that another
-            # rank's producing kernel needs, and the challenge never comes.
-            # Launch each step after its challenge instead (same proof).
-            os.environ["ZK_PRELAUNCH"] = "0"  # read at zk_ctx_create
-        local = local % ndev
+        # (the library launches each step after its challenge with a host
+        # all-reduce, so ranks that share a card cannot starve each other)
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     if args.force_rccl and world == 1:
         os.environ["ZK_FORCE_COLLECTIVES"] = "1"  # read at zk_ctx_create

@@ -321,7 +321,10 @@ int zk_dev_gkr_sumcheck_prove(zk_ctx* ctx, zk_field field, const void* const d_t
  * No broadcast is needed: every rank derives the same challenges from the
  * same transcript.
  * ------------------------------------------------------------------------- */
-/* host-memory all-reduce supplied by the caller (e.g. torch.distributed/gloo) */
+/* host-memory all-reduce supplied by the caller (e.g. torch.distributed/gloo).
+ * With a host callback attached every step launches after its challenge
+ * (pre-enqueue off): the callback's latency is unbounded and ranks may share
+ * one device. */
 typedef int (*zk_allreduce_u64_fn)(void* user, uint64_t* data, size_t count); /* in-place SUM, 0 = ok */
 int zk_ctx_attach_host_comm(zk_ctx* ctx, int rank, int world, zk_allreduce_u64_fn allreduce, void* user);
 /* RCCL over xGMI: rank 0 creates the id, every rank passes the same 128 bytes */

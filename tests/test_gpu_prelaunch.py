@@ -128,7 +128,7 @@ def test_first_double_step_matches_oracle(monkeypatch, field, n):
     runs round 0 alone and round 1 as a single step. Both equal the oracle, pre-enqueued
     and per-round launched."""
     want = _oracle(field, n)
-    for d0 in ("1", "2", "0"):  # 1: k_gkr_d0r (3 lanes per quad-product, default), 2: k_gkr_d0 (8 lanes)
+    for d0 in ("3", "1", "2", "0"):  # 3: k_gkr_d0m (matrix cores), 1: k_gkr_d0r (3 lanes per quad-product), 2: k_gkr_d0 (8 lanes)
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_D0", d0)
             monkeypatch.setenv("ZK_PRELAUNCH", pre)
@@ -143,14 +143,14 @@ def test_first_double_step_matches_oracle(monkeypatch, field, n):
 def test_first_double_step_agrees_22var(monkeypatch, field):
     n = 22
     got = {}
-    for d0 in ("1", "2", "0"):
+    for d0 in ("3", "1", "2", "0"):
         monkeypatch.setenv("ZK_D0", d0)
         ctx = zk_amd.Context(0)
         try:
             got[d0] = _prove(ctx, field, n)
         finally:
             ctx.close()
-    assert got["1"] == got["0"] == got["2"]
+    assert got["3"] == got["1"] == got["0"] == got["2"]
 
 
 @pytest.mark.parametrize("field", [0, 2])

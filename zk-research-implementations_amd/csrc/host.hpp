@@ -22,6 +22,7 @@
 #include "field.hpp"
 #include "keccak.hpp"
 #include "kernels.hpp"
+#include "mfma.hpp"
 #include "hfield.hpp"
 
 using zk::Fe;
@@ -202,7 +203,7 @@ struct zk_ctx {
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
-  int d0 = 1;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
+  int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
@@ -485,8 +486,13 @@ struct PostR {
   }
 };
 
-// Pre-enqueue the rounds of a phase (ZK_PRELAUNCH, default on)?
-inline bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1; }
+// Pre-enqueue the rounds of a phase (ZK_PRELAUNCH, default on)? Never with a
+// host all-reduce callback (zk_ctx_attach_host_comm): the callback's latency is
+// unbounded (a lagging rank would trip the kernels' 1 s challenge guard), and
+// ranks that share one device would starve each other — a pre-enqueued step
+// spinning on its challenge holds the CUs the other rank's producing kernel
+// needs. Each step then launches after its challenge (same proof).
+inline bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1 && c->comm != COMM_HOST; }
 
 // Run `nv` rounds over 4 device tables of 2^nv elements starting at global
 // round k0, as a sequence of steps:
@@ -599,7 +605,12 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     if (st.kind == GS_D0) {  // rounds 0 and 1 over the input tables (size 4Q), nothing written
       const uint64_t Q = size / 4;
-      if (c->d0 == 2) {  // ZK_D0=2: the 8-lane k_gkr_d0 (DPP exchange, V11 in schoolbook rows)
+      if (c->d0 == 3) {  // products on the matrix cores (k_gkr_d0m, mfma.hpp)
+        const uint64_t nch = (Q + 31) / 32;
+        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_d0m<F>);
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + 2 * zk::kD0MChunksMax - 1) / (2 * zk::kD0MChunksMax));
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0m<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
+      } else if (c->d0 == 2) {  // ZK_D0=2: the 8-lane k_gkr_d0 (DPP exchange, V11 in schoolbook rows)
         const uint32_t grid = grid_for(c, zk::kDQuads * Q, zk::k_gkr_d0<F>);
         launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
       } else {  // a quad-product per three lanes, one grid row each (k_gkr_d0r)

@@ -17,6 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
+ABI_VERSION = 9  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
 KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0"]
 
 
@@ -127,6 +128,14 @@ def lib():
         except ImportError:
             pass
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        L.zk_abi_version.restype = C.c_uint32
+        L.zk_abi_version.argtypes = []
+        got = L.zk_abi_version()
+        if got != ABI_VERSION:
+            raise ImportError(
+                f"{LIB_PATH} has ABI version {got}, this binding expects {ABI_VERSION} "
+                f"(stale build?): rebuild it with `make -C {PKG_ROOT}`"
+            )
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
