@@ -191,3 +191,39 @@ def test_host_failure_mid_proof_releases_waiting_rounds(monkeypatch):
         assert _prove(ctx, 0, 14) == _oracle(0, 14)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("n", [10, 13, 16])
+def test_matrix_core_double_steps_match_oracle(monkeypatch, field, n):
+    """Double steps with two pending challenges on the matrix cores (k_gkr_dm,
+    mfma.hpp: fold by (ra, rb) as a K = 96 int8 MFMA + REDC, grid-point
+    products as K = 64 MFMAs) give the oracle's proof; ZK_DM_MIN_QUADS=64 puts
+    every double step with >= 64 quads on it (n = 13: after round 0 and a
+    single round, so its first double step has one pending challenge and
+    stays on k_gkr_dround)."""
+    want = _oracle(field, n)
+    monkeypatch.setenv("ZK_DM_MIN_QUADS", "64")
+    for dm in ("1", "0"):
+        for pre in ("1", "0"):
+            monkeypatch.setenv("ZK_DM", dm)
+            monkeypatch.setenv("ZK_PRELAUNCH", pre)
+            ctx = zk_amd.Context(0)
+            try:
+                assert _prove(ctx, field, n) == want, f"ZK_DM={dm} ZK_PRELAUNCH={pre}"
+            finally:
+                ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 2])
+def test_matrix_core_double_steps_agree_22var(monkeypatch, field):
+    n = 22
+    got = {}
+    for dm in ("1", "0"):
+        monkeypatch.setenv("ZK_DM", dm)
+        ctx = zk_amd.Context(0)
+        try:
+            got[dm] = _prove(ctx, field, n)
+        finally:
+            ctx.close()
+    assert got["1"] == got["0"]

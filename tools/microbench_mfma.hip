@@ -3,6 +3,10 @@
 //   1. v_mfma_i32_32x32x32_i8 operand maps: which lane/byte holds A[i][k] and
 //      B[k][j] (two hypotheses, checked with random int8 data against the CPU).
 //   2. ds_read_b64_tr_b8: which LDS byte lands in which lane/byte (dump).
+//   4. v_permlane32_swap: what __builtin_amdgcn_permlane32_swap(x, x) returns.
+//   5. k_dm_pattern: the memory side of k_gkr_dm alone (per wave: one table, per
+//      64-quad chunk and corner four loads at quarter offsets + one store; xor
+//      instead of arithmetic) at the 24-variable first double step (Q = 2^20).
 //   3. k_dot: sum_j A_j * S_j over 256-bit values through signed 8-bit digits,
 //      an LDS row image, transposed reads and the i8 MFMA, checked exactly
 //      against a CPU big-integer sum, and timed at 2^24 elements per table.
@@ -46,6 +50,36 @@ __global__ void k_tr8_probe(v2i* out, int mode) {
   int addr = mode == 0 ? 8 * l : 8 * (l ^ 1);
   v2i r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(lds + addr));
   out[l] = r;
+}
+
+// ---- 4. permlane32_swap probe
+__global__ void k_swap_probe(int* out) {
+  const int l = threadIdx.x;
+  auto r = __builtin_amdgcn_permlane32_swap(l, l, false, false);
+  out[2 * l] = r[0];
+  out[2 * l + 1] = r[1];
+}
+
+// ---- 5. memory-only k_gkr_dm pattern
+__global__ __launch_bounds__(256) void k_dm_pattern(const uint4* const* in, uint4* const* out, size_t Q) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* X = in[w];
+  uint4* X2 = out[w];
+  const size_t nch = Q / 64, h4 = 4 * Q;
+  for (size_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const size_t j = ch * 64 + l;
+    for (int k = 0; k < 4; ++k) {
+      const size_t i = j + k * Q;
+      uint4 a = X[2 * i], b = X[2 * i + 1];
+      for (int q = 1; q < 4; ++q) {
+        const uint4 c = X[2 * (i + q * h4)], d = X[2 * (i + q * h4) + 1];
+        a.x ^= c.x; a.y ^= c.y; a.z ^= c.z; a.w ^= c.w;
+        b.x ^= d.x; b.y ^= d.y; b.z ^= d.z; b.w ^= d.w;
+      }
+      X2[2 * i] = a;
+      X2[2 * i + 1] = b;
+    }
+  }
 }
 
 // ---- 3. exact dot product through the matrix cores
@@ -192,6 +226,21 @@ int main() {
       }
     }
   }
+  // ---- 4
+  {
+    int* d;
+    CK(hipMalloc(&d, 128 * 4));
+    k_swap_probe<<<1, 64>>>(d);
+    int h[128];
+    CK(hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost));
+    int ok = 1;
+    for (int l = 0; l < 64; ++l) {
+      const int partner = l ^ 32, want0 = l < 32 ? l : partner, want1 = l < 32 ? partner : l;
+      ok &= h[2 * l] == want0 && h[2 * l + 1] == want1;
+    }
+    printf("permlane32_swap(x, x) = {lanes<32: own, else partner ; lanes<32: partner, else own}: %s (lane 0: %d %d, lane 40: %d %d)\n",
+           ok ? "yes" : "NO", h[0], h[1], h[80], h[81]);
+  }
   // ---- 3
   {
     const size_t n = (size_t)1 << 24;
@@ -236,6 +285,37 @@ int main() {
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= iters;
     printf("k_dot 2^24 x 2 tables: %.1f us, %.2f TB/s\n", ms * 1e3, n * 64.0 / (ms * 1e-3) / 1e12);
+  }
+  // ---- 5
+  {
+    const size_t Q = (size_t)1 << 20;
+    uint4 *hin[4], *hout[4];
+    for (int t = 0; t < 4; ++t) {
+      CK(hipMalloc(&hin[t], 16 * Q * 32));
+      CK(hipMalloc(&hout[t], 4 * Q * 32));
+      CK(hipMemset(hin[t], t + 1, 16 * Q * 32));
+    }
+    const uint4** din;
+    uint4** dout;
+    CK(hipMalloc(&din, sizeof hin));
+    CK(hipMalloc(&dout, sizeof hout));
+    CK(hipMemcpy(din, hin, sizeof hin, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dout, hout, sizeof hout, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int grid : {512, 768, 1024, 2048}) {
+      for (int it = 0; it < 2; ++it) k_dm_pattern<<<grid, 256>>>(din, dout, Q);
+      CK(hipEventRecord(e0));
+      for (int it = 0; it < 5; ++it) k_dm_pattern<<<grid, 256>>>(din, dout, Q);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double bytes = 4.0 * (16 * Q + 4 * Q) * 32;
+      printf("k_dm_pattern Q=2^20 grid %d: %.1f us, %.2f TB/s (%.2f GB)\n", grid, ms * 1e3, bytes / (ms * 1e-3) / 1e12, bytes / 1e9);
+    }
   }
   return 0;
 }

@@ -204,6 +204,8 @@ struct zk_ctx {
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
   int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
+  bool dm = true;           // double steps with two pending challenges on the matrix cores (k_gkr_dm; ZK_DM=0: k_gkr_dround)
+  uint64_t dm_min_quads = 1u << 17;  // ... when they have at least this many quads (ZK_DM_MIN_QUADS; smaller steps are latency-bound: k_gkr_dround)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
@@ -695,9 +697,19 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       } else {
         din.rb = rb;
       }
+      const double bytes = (st.np == 2 ? 2560.0 : 1536.0) * Q, muls = (st.np == 2 ? 40.0 : 24.0) * Q;
+      if (st.np == 2 && c->dm && Q >= std::max<uint64_t>(c->dm_min_quads, zk::kDMQuads)) {  // matrix cores (mfma.hpp)
+        const uint64_t nch = Q / zk::kDMQuads;
+        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_dm<F>);
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
+        launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dm<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1],
+               nx[2], nx[3], Q, din, sk);
+        for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+        enqueue_reduce(c, sk, across_ranks, zk::kDLimbs);
+        return;
+      }
       const uint32_t grid = st.np == 2 ? grid_for(c, zk::kDQuads * Q, zk::k_gkr_dround<F, 2>)
                                        : grid_for(c, zk::kDQuads * Q, zk::k_gkr_dround<F, 1>);
-      const double bytes = (st.np == 2 ? 2560.0 : 1536.0) * Q, muls = (st.np == 2 ? 40.0 : 24.0) * Q;
       if (st.np == 2)
         launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dround<F, 2>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
                nx[1], nx[2], nx[3], Q, din, sk);

@@ -225,4 +225,290 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0m(const Fe* __restrict__ A,
   grid_finish<kD0Limbs>(sc, sink);
 }
 
+
+// ---------------------------------------------------------------------------
+// Double steps on the matrix cores: k_gkr_dm (two pending challenges).
+//
+// The step of k_gkr_dround<F, 2> (kernels.hpp): fold the level-(i-2) tables
+// by (ra, rb) at once, write level i, and sum the eight grid-point products
+// of rounds i and i+1 over level i's quads. Both halves are contractions:
+//
+// Fold. Z = x00 + ra d1 + rb d2 + rab d3 (fold2, field.hpp) with
+// d1 = x10 - x00, d2 = x01 - x00, d3 = x11 - x01 - d1. With the step
+// constants w_c[k] = r_c 2^(8k + 64) mod p (c = ra, rb, rab; k = 0..31) and
+// the signed digits delta_{c,k} of d_c,
+//   Y = sum_{c,k} delta_{c,k} w_c[k] == (ra d1 + rb d2 + rab d3) 2^64 (mod p),
+// and digit position pos of Y is sum_{c,k} w_c[k]_pos delta_{c,k}: an
+// MFMA with A = the constants' digits (rows pos, k = (c, k)) and B = the
+// differences' digits (k = (c, k), columns = 32 elements), K = 96. Column e
+// of the int32 result is element e's 32 position sums (|.| < 2^21), split
+// over lanes e and e + 32 (even / odd 32-bit words); the lanes assemble
+// signed 64-bit word sums, trade halves with v_permlane32_swap, propagate
+// carries, run two 32-bit REDC steps (the 2^64) and add x00: Z fully
+// reduced. The 3 x 96 constants' digit rows are built once per block.
+//
+// Products. As k_gkr_d0m: lane l holds the four folded corners of quad
+// j0 + l of its wave's table (wave w: table w = A, S, M, P), forms the
+// eight grid-point values (categories of kernels.hpp: 0 V00, 1 V22, 2 V01,
+// 3 V02, 4 V10, 5 V20, 6 V21, 7 V12) and writes their digit rows into a
+// block image [category][table][64 quads]; after a barrier wave w runs the
+// products of pair w & 1 (A*S or M*P) for categories 4 (w >> 1) .. +3, two
+// K = 32 MFMAs each. Epilogue and limb sums as k_gkr_d0m (8 categories).
+// ---------------------------------------------------------------------------
+#define ZK_P2D8(F, b) pow2_mod_p<F>(b), pow2_mod_p<F>(b + 8), pow2_mod_p<F>(b + 16), pow2_mod_p<F>(b + 24)
+#define ZK_P2D_INIT(F)                                                                                             \
+  {ZK_P2D8(F, 64), ZK_P2D8(F, 96), ZK_P2D8(F, 128), ZK_P2D8(F, 160), ZK_P2D8(F, 192), ZK_P2D8(F, 224),             \
+   ZK_P2D8(F, 256), ZK_P2D8(F, 288)}
+static __constant__ Fe kP2DBn254Fr[32] = ZK_P2D_INIT(Bn254Fr);
+static __constant__ Fe kP2DBn254Fq[32] = ZK_P2D_INIT(Bn254Fq);
+static __constant__ Fe kP2DBls12_381Fr[32] = ZK_P2D_INIT(Bls12_381Fr);
+template <class F>
+__device__ __forceinline__ Fe p2dig(uint32_t k) {  // 2^(8k + 64) mod p
+  if constexpr (F::id == BN254_FR) return kP2DBn254Fr[k];
+  else if constexpr (F::id == BN254_FQ) return kP2DBn254Fq[k];
+  else return kP2DBls12_381Fr[k];
+}
+
+// the partner lane's value (lane l <-> l ^ 32; v_permlane32_swap, tools/microbench_mfma.hip)
+__device__ __forceinline__ uint32_t xchg32(uint32_t x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (threadIdx.x & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ Fe sub256(const Fe& a, const Fe& b) {  // two's complement a - b
+  Fe r;
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = subb32(a.v[i], b.v[i], bw, &bw);
+  return r;
+}
+// signed 64-bit sum of four int32 byte-position sums at byte offsets 0, 8, 16, 24
+__device__ __forceinline__ int64_t word_of(int a0, int a1, int a2, int a3) {
+  return (int64_t)a0 + ((int64_t)a1 << 8) + ((int64_t)a2 << 16) + ((int64_t)a3 << 24);
+}
+
+// Z = x00 + Y 2^-64 (mod p), Y = sum_i W[i] 2^(32 i) (signed words, |Y| < 2^271)
+template <class F>
+__device__ __forceinline__ Fe dm_finish(const int64_t (&W)[8], const Fe& x00) {
+  uint32_t y[8];
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t v = W[i] + c;
+    y[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  int64_t top = c;  // Y = y + top 2^256
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {  // REDC by 2^32: (Y + m p) / 2^32, exact
+    const uint32_t m = y[0] * F::PINV;
+    uint64_t a = (uint64_t)m * F::P[0] + y[0];
+    uint32_t cc = (uint32_t)(a >> 32);
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      a = (uint64_t)m * F::P[j] + y[j] + cc;
+      y[j - 1] = (uint32_t)a;
+      cc = (uint32_t)(a >> 32);
+    }
+    const int64_t tt = top + cc;
+    y[7] = (uint32_t)tt;
+    top = tt >> 32;
+  }
+  // V = y + top 2^256 in (-2^208, p + 2^208); x00 + V + p in (0, 3p + 2^208): two conditional subtractions
+  Fe s;
+  uint32_t c1 = 0, c2 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.v[i] = addc32(y[i], x00.v[i], c1, &c1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.v[i] = addc32(s.v[i], F::P[i], c2, &c2);
+  int32_t hi = (int32_t)top + (int32_t)c1 + (int32_t)c2;  // 0 or 1
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    Fe t;
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t q = pass == 0 ? ((F::P[i] << 1) | (i ? F::P[i - 1] >> 31 : 0u)) : F::P[i];
+      t.v[i] = subb32(s.v[i], q, b, &b);
+    }
+    const int32_t th = hi - (int32_t)b;
+    const bool take = th >= 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.v[i] = take ? t.v[i] : s.v[i];
+    hi = take ? th : hi;
+  }
+  return s;
+}
+
+// fold element i of one table (level-(i-2) inputs at i, i + h4, i + 2 h4, i + 3 h4) by
+// (ra, rb, rab); every lane folds its own element, wf[c] = the A fragments of the constants
+__device__ __forceinline__ void dm_load(const Fe* __restrict__ X, uint64_t i, uint64_t h4, Fe (&x)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = ld_fe(X, i + k * h4);  // x00, x01, x10, x11
+}
+template <class F>
+__device__ __forceinline__ Fe dm_fold(const Fe (&x)[4], const i32x4 (&wf)[3]) {
+  const Fe &x00 = x[0], &x01 = x[1], &x10 = x[2], &x11 = x[3];
+  Fe d[3];
+  if constexpr (kLazyDigits<F>) {  // signed differences, |d1|, |d2| < p, |d3| < 2p
+    d[0] = sub256(x10, x00);
+    d[1] = sub256(x01, x00);
+    d[2] = sub256(sub256(x11, x01), d[0]);
+  } else {
+    d[0] = fe_sub<F>(x10, x00);
+    d[1] = fe_sub<F>(x01, x00);
+    d[2] = fe_sub<F>(fe_sub<F>(x11, x01), d[0]);
+  }
+  const bool h = (threadIdx.x & 32) != 0;
+  i32x16 acc0, acc1;  // columns: elements j0 .. j0+31 (acc0), j0+32 .. j0+63 (acc1)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    to_digits(d[c]);
+    // B fragment of lane (e, h): digits 16h .. 16h+15 of element e (acc0) / 32 + e (acc1);
+    // lane e owns element e, lane e + 32 element 32 + e: trade the half the partner needs
+    i32x4 own_lo, own_hi, got;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      own_lo[q] = (int)d[c].v[q];
+      own_hi[q] = (int)d[c].v[4 + q];
+      got[q] = (int)xchg32(h ? d[c].v[q] : d[c].v[4 + q]);
+    }
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? got : own_lo, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? own_hi : got, acc1, 0, 0, 0);
+  }
+  // lane (e, h) holds words 2g + h (g = 0..3) of both columns; it keeps its own element's
+  // (acc0 for h = 0, acc1 for h = 1) and sends the partner's
+  int64_t W[8];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int64_t keep = h ? word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3])
+                           : word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
+    const int64_t send = h ? word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3])
+                           : word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
+    const uint32_t lo = xchg32((uint32_t)send), hi = xchg32((uint32_t)((uint64_t)send >> 32));
+    const int64_t recv = (int64_t)(((uint64_t)hi << 32) | lo);
+    W[2 * g] = h ? recv : keep;
+    W[2 * g + 1] = h ? keep : recv;
+  }
+  return dm_finish<F>(W, x00);
+}
+
+constexpr uint32_t kDMQuads = 64;        // quads per chunk (one per lane)
+constexpr uint32_t kDMChunksMax = 1024;  // chunks per block (int32 product tiles: 2^20 per chunk)
+struct DMScratch {
+  uint8_t img[kDCats][4][kDMQuads][32];  // 64 KB: category, table, quad, digit row
+  uint8_t wimg[3][32][32];                // digit rows of the fold constants (c, k)
+  unsigned long long T[kDCats][64];
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+};
+
+template <class F>
+__device__ __forceinline__ void dm_row(uint8_t (&row)[32], Fe x) {
+  to_digits(x);
+  st_row(row, x);
+}
+
+// G + M -> 17 words for category t (threads < ncat), as k_gkr_d0m
+template <class F>
+__device__ __forceinline__ void diag_to_words(const unsigned long long (&T)[64], uint64_t* out) {
+  int64_t carry = 0;
+  uint32_t word = 0;
+  for (int d = 0; d < 68; ++d) {
+    const int wd = d >> 2, sh = 8 * (d & 3);
+    int64_t s = carry + (d < 63 ? (int64_t)T[d] : 0);
+    s += (int64_t)((d0m_offset_word<F>(wd) >> sh) & 0xffu);
+    word |= (uint32_t)(s & 0xff) << sh;
+    carry = s >> 8;
+    if ((d & 3) == 3) {
+      out[wd] = word;
+      word = 0;
+    }
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                     const Fe* __restrict__ M, const Fe* __restrict__ P,
+                                                     Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
+                                                     Fe* __restrict__ P2, uint64_t Q, DIn din, RoundSink sink) {
+  Fe ra, rb, rab;
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  block_get_rs(din, ra, rb, rab, gridDim.x > 1);
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
+  __shared__ DMScratch sc;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, pp = w & 1, cg = w >> 1;
+  if (t < 96) {
+    const uint32_t c = t >> 5, k = t & 31;
+    dm_row<F>(sc.wimg[c][k], fe_mul<F>(c == 0 ? ra : (c == 1 ? rb : rab), p2dig<F>(k)));
+  }
+  for (uint32_t i = t; i < kDCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  __syncthreads();
+  i32x4 wf[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) wf[c] = tr_frag(&sc.wimg[c][0][0]);
+  const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
+  Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
+  i32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0;
+  const uint64_t nch = Q / kDMQuads, h4 = 4 * Q;
+  Fe in[4];  // inputs of the next fold, loaded one fold ahead
+  if ((uint64_t)blockIdx.x < nch) dm_load(X, (uint64_t)blockIdx.x * kDMQuads + l, h4, in);
+  for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const uint64_t j = ch * kDMQuads + l;
+    Fe z[4];  // corners V(a, b) = Z[j + (2a + b) Q]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      Fe cur[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[q] = in[q];
+      if (k < 3)
+        dm_load(X, j + (k + 1) * Q, h4, in);
+      else if (ch + gridDim.x < nch)
+        dm_load(X, (ch + gridDim.x) * kDMQuads + l, h4, in);
+      z[k] = dm_fold<F>(cur, wf);
+      st_fold(X2, j + k * Q, z[k]);
+    }
+    const Fe v20 = at2<F>(z[0], z[2]), v21 = at2<F>(z[1], z[3]);  // reduced
+    dm_row<F>(sc.img[0][w][l], z[0]);
+    dm_row<F>(sc.img[2][w][l], z[1]);
+    dm_row<F>(sc.img[4][w][l], z[2]);
+    dm_row<F>(sc.img[3][w][l], kLazyDigits<F> ? lazy2(z[0], z[1]) : at2<F>(z[0], z[1]));
+    dm_row<F>(sc.img[7][w][l], kLazyDigits<F> ? lazy2(z[2], z[3]) : at2<F>(z[2], z[3]));
+    dm_row<F>(sc.img[5][w][l], v20);
+    dm_row<F>(sc.img[6][w][l], v21);
+    dm_row<F>(sc.img[1][w][l], kLazyDigits<F> ? lazy2(v20, v21) : at2<F>(v20, v21));
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t cat = 4 * cg + i;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const i32x4 fa = tr_frag(&sc.img[cat][2 * pp][32 * half][0]);
+        const i32x4 fb = tr_frag(&sc.img[cat][2 * pp + 1][32 * half][0]);
+        acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb, acc[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t col = l & 31, h = l >> 5;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      atomicAdd(&sc.T[4 * cg + i][row + col], (unsigned long long)(long long)acc[i][r]);
+    }
+  }
+  __syncthreads();
+  if (t < (uint32_t)kDCats) diag_to_words<F>(sc.T[t], sc.tot + t * 17);
+  __syncthreads();
+  grid_finish<kDLimbs>(sc, sink);
+}
+
 }  // namespace zk
