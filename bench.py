@@ -418,7 +418,7 @@ def main() -> None:
             # during the LAST timed step only: their marker packets cost the GPU
             # ~5 us per round, so timing every step would inflate ms_per_step
             st0 = ctx.stats()
-            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0"])
+            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm"])
         step()
     torch.cuda.synchronize()
     barrier()
@@ -436,14 +436,17 @@ def main() -> None:
     ms_per_step = elapsed * 1e3 / args.steps
     k = st["kernels"]
     # per kernel kind over the event-timed (last) step; the dominant kernel is
-    # k_gkr_round (round 1: the longest launch of the proof)
+    # the kind with the most time in the proof (k_gkr_dm at n = 24)
     def kind(name):
         d = {f: k[name][f] - st0["kernels"][name][f] for f in ("launches", "alg_bytes")}
         d["ms"] = k[name]["ms"]
         return d
 
     round_kinds = {
-        "gkr_d0": "k_gkr_d0r (rounds 0 and 1 in one pass over the input tables: nine grid-point product sums, nothing written)",
+        "gkr_d0": "k_gkr_d0m (rounds 0 and 1 in one pass over the input tables: nine grid-point product sums "
+                  "on the int8 matrix cores, nothing written)",
+        "gkr_dm": "k_gkr_dm (double steps with >= 2^17 quads on the int8 matrix cores: fold the level-(i-2) "
+                  "tables by (r_a, r_b), write level i, eight grid-point product sums)",
         "gkr_round0": "k_gkr_round0 (round 0: e0, e1, e2 over the input tables)",
         "gkr_round": "k_gkr_round (round 1: fold by r0 + round sums)",
         "gkr_round_lanes": "k_gkr_round_lanes (single small rounds, 8 lanes per pair)",
@@ -458,9 +461,9 @@ def main() -> None:
             per_kind[name] = {"kernel": desc, "launches": d["launches"], "ms": d["ms"],
                               "alg_GB": d["alg_bytes"] / 1e9,
                               "achieved_GBs": d["alg_bytes"] / (d["ms"] / 1e3) / 1e9 if d["ms"] else None}
-    # the dominant kernel: the kind with the longest average launch (k_gkr_d0r with
-    # ZK_D0 on, k_gkr_round — round 1 — with it off)
-    dom = max(per_kind, key=lambda nm: per_kind[nm]["ms"] / per_kind[nm]["launches"])
+    # the dominant kernel: the kind with the most time in the timed proof
+    # (k_gkr_dm at n = 24: the first two double steps)
+    dom = max(per_kind, key=lambda nm: per_kind[nm]["ms"])
     rnd = kind(dom)
     all_b = sum(kind(nm)["alg_bytes"] for nm in per_kind)
     all_ms = sum(kind(nm)["ms"] for nm in per_kind)
@@ -469,12 +472,12 @@ def main() -> None:
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
 
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "r1_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r2_traffic.json")
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
         if t.get("kind") == dom and field == 0:  # per-symbol summary of this workload
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
-            traffic_src = f"profiles/r1_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
+            traffic_src = f"profiles/r2_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
     if rank == 0:
         out = {
@@ -502,10 +505,10 @@ def main() -> None:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": round_kinds[dom] + "; the longest launch",
-                "bound_note": "k_gkr_d0r is VALU-bound (multiply issue: nine unreduced 256-bit products per "
-                "quad and table pair), so its HBM fraction is below round 1's; the proof is faster with it "
-                "(DESIGN.md section 3)" if dom == "gkr_d0" else None,
+                "kernel": round_kinds[dom] + "; the kind with the most time in the proof",
+                "bound_note": "HBM: the field products run on the int8 matrix cores (DESIGN.md section 3); the "
+                "same access pattern with xor instead of arithmetic reaches 5.3-5.5 TB/s "
+                "(tools/microbench_mfma.hip k_dm_pattern, profiles/r2_mb_mfma.txt)" if dom == "gkr_dm" else None,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 9u
+#define ZK_ABI_VERSION 10u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -81,8 +81,9 @@ enum {
   ZK_K_GKR_TAIL = 10,  /* the small rounds of a proof in one persistent kernel (k_gkr_tail, ZK_DROUND=0) */
   ZK_K_GKR_DROUND = 11, /* two rounds per kernel: pending folds + round sums + next round's quadratics (k_gkr_dround) */
   ZK_K_GKR_DTAIL = 12, /* the small double rounds in one persistent kernel (k_gkr_dtail) */
-  ZK_K_GKR_D0 = 13,    /* rounds 0 and 1 in one pass over the input tables (k_gkr_d0r / k_gkr_d0) */
-  ZK_K_KINDS = 14
+  ZK_K_GKR_D0 = 13,    /* rounds 0 and 1 in one pass over the input tables (k_gkr_d0m on the matrix cores; k_gkr_d0r / k_gkr_d0) */
+  ZK_K_GKR_DM = 14,    /* double steps with two pending challenges on the matrix cores (k_gkr_dm) */
+  ZK_K_KINDS = 15
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];

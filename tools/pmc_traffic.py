@@ -7,7 +7,8 @@ bytes (the x2 is the gfx950 correction for wide coalesced streaming reads,
 MI355X_MICROARCH.md "HBM") beside the algorithmic bytes of the step schedule
 (host.hpp gkr_phase): round 0 256 B per pair, a single round 768 B per output
 pair, a double step 1536 B (one pending challenge) or 2560 B (two) per quad,
-the persistent tail the sum of its double steps.
+the persistent tail the sum of its double steps; k_gkr_d0m 128 B per input
+index, k_gkr_dm 2560 B per quad.
 Writes profiles/<tag>_traffic.json and copies the kernel-stats CSV.
 usage: python tools/pmc_traffic.py <tag> <nvars> [dtail_max_quads]
 (tools/profile_bench.sh launches steps one at a time, ZK_PRELAUNCH=0: no persistent
@@ -28,12 +29,13 @@ def dispatches(path, counter):
     return [out[k] for k in sorted(out)]
 
 
-def schedule(n, dtail_max_quads=4096, d0=True):
-    """(symbol prefix, algorithmic bytes) per dispatch of one proof (pre-enqueued, one GPU).
-    d0 (ZK_D0, default): an even n starts with k_gkr_d0r (rounds 0 and 1, 128 B per
-    input index) and every double step then folds by two pending challenges."""
+def schedule(n, dtail_max_quads=4096, d0=True, dm_min_quads=1 << 17):
+    """(symbol prefix, algorithmic bytes) per dispatch of one proof (one GPU).
+    d0 (ZK_D0, default): an even n starts with k_gkr_d0m (rounds 0 and 1, 128 B per
+    input index) and every double step then folds by two pending challenges; those
+    with >= dm_min_quads quads run as k_gkr_dm (matrix cores), the others as k_gkr_dround."""
     if d0 and n >= 2 and n % 2 == 0:
-        st = [("zk::k_gkr_d0r", 128.0 * (1 << n))]
+        st = [("zk::k_gkr_d0m", 128.0 * (1 << n))]
         i, np_ = 2, 2
     else:
         st = [("zk::k_gkr_round0", 256.0 * (1 << (n - 1)))]
@@ -53,7 +55,8 @@ def schedule(n, dtail_max_quads=4096, d0=True):
     if len(doubles) - d0 < 2:
         d0 = len(doubles)
     for q, p in doubles[:d0]:
-        st.append((f"zk::k_gkr_dround<zk::Bn254Fr, {p}>", (1536.0 if p == 1 else 2560.0) * q))
+        sym = "zk::k_gkr_dm" if p == 2 and q >= dm_min_quads else f"zk::k_gkr_dround<zk::Bn254Fr, {p}>"
+        st.append((sym, (1536.0 if p == 1 else 2560.0) * q))
     if d0 < len(doubles):
         st.append(("zk::k_gkr_dtail", sum((1536.0 if p == 1 else 2560.0) * q for q, p in doubles[d0:])))
     return st
@@ -87,12 +90,13 @@ def main():
         return {"launches": len(rs), "traffic_bytes_per_launch": t / max(1, len(rs)),
                 "alg_bytes_per_launch": a / max(1, len(rs)), "traffic_over_alg": t / a if a else None}
 
-    if first == "zk::k_gkr_d0r":  # the longest launch of the proof (bench.py's dominant kernel)
-        big, name, kind = summary(lambda k: k.startswith(first)), "k_gkr_d0r", "gkr_d0"
+    if any(sym == "zk::k_gkr_dm" for sym, _ in sched):  # the kind with the most time (bench.py's dominant kernel)
+        big, name, kind = summary(lambda k: k.startswith("zk::k_gkr_dm")), "k_gkr_dm", "gkr_dm"
     else:
-        big, name, kind = summary(lambda k: k.startswith("zk::k_gkr_round<")), "k_gkr_round", "gkr_round"
+        big, name, kind = summary(lambda k: k.startswith(first)), first[4:], "gkr_d0"
     res = {"kernel": name, "kind": kind, "nvars": nvars, **big,
-           "others": {"k_gkr_round0": summary(lambda k: "k_gkr_round0" in k),
+           "others": {"k_gkr_d0m": summary(lambda k: "k_gkr_d0m" in k),
+                      "k_gkr_round0": summary(lambda k: "k_gkr_round0" in k),
                       "k_gkr_round": summary(lambda k: k.startswith("zk::k_gkr_round<")),
                       "k_gkr_dround": summary(lambda k: "k_gkr_dround" in k),
                       "k_gkr_dtail": summary(lambda k: "k_gkr_dtail" in k)},

@@ -702,7 +702,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         const uint64_t nch = Q / zk::kDMQuads;
         const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_dm<F>);
         const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
-        launch(c, ZK_K_GKR_DROUND, bytes, muls, zk::k_gkr_dm<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1],
+        launch(c, ZK_K_GKR_DM, bytes, muls, zk::k_gkr_dm<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1],
                nx[2], nx[3], Q, din, sk);
         for (int t = 0; t < 4; ++t) cur[t] = nx[t];
         enqueue_reduce(c, sk, across_ranks, zk::kDLimbs);
