@@ -128,6 +128,7 @@ def test_first_double_step_matches_oracle(monkeypatch, field, n):
     runs round 0 alone and round 1 as a single step. Both equal the oracle, pre-enqueued
     and per-round launched."""
     want = _oracle(field, n)
+    monkeypatch.setenv("ZK_D0T", "0")  # the two-round first pass (even n >= 14 default to three rounds)
     for d0 in ("3", "1", "2", "0"):  # 3: k_gkr_d0m (matrix cores), 1: k_gkr_d0r (3 lanes per quad-product), 2: k_gkr_d0 (8 lanes)
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_D0", d0)
@@ -143,6 +144,7 @@ def test_first_double_step_matches_oracle(monkeypatch, field, n):
 def test_first_double_step_agrees_22var(monkeypatch, field):
     n = 22
     got = {}
+    monkeypatch.setenv("ZK_D0T", "0")
     for d0 in ("3", "1", "2", "0"):
         monkeypatch.setenv("ZK_D0", d0)
         ctx = zk_amd.Context(0)
@@ -204,6 +206,7 @@ def test_matrix_core_double_steps_match_oracle(monkeypatch, field, n):
     stays on k_gkr_dround)."""
     want = _oracle(field, n)
     monkeypatch.setenv("ZK_DM_MIN_QUADS", "64")
+    monkeypatch.setenv("ZK_D0T", "0")
     for dm in ("1", "0"):
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_DM", dm)
@@ -219,11 +222,48 @@ def test_matrix_core_double_steps_match_oracle(monkeypatch, field, n):
 def test_matrix_core_double_steps_agree_22var(monkeypatch, field):
     n = 22
     got = {}
+    monkeypatch.setenv("ZK_D0T", "0")
     for dm in ("1", "0"):
         monkeypatch.setenv("ZK_DM", dm)
         ctx = zk_amd.Context(0)
         try:
             got[dm] = _prove(ctx, field, n)
+        finally:
+            ctx.close()
+    assert got["1"] == got["0"]
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("n", [11, 13, 14, 15, 16, 18])
+def test_three_round_first_pass_matches_oracle(monkeypatch, field, n):
+    """Rounds 0-2 in one pass over the inputs (k_gkr_d0t: 27 moment tiles of
+    corner-pair products on the matrix cores), then the inputs folded by
+    (r0, r1, r2) at once (eq weights, K = 256): odd n >= 11 run rounds 3-4
+    there (k_gkr_dm3), even n >= 14 rounds 3-5 (k_gkr_t33: 27 moment tiles
+    over the folded octants) and fold by three once more for rounds 6-7
+    (k_gkr_dm3); double steps follow. ZK_D0T=0 keeps the two-round first
+    pass. Both give the oracle's proof, pre-enqueued and launched per step."""
+    want = _oracle(field, n)
+    for d0t in ("1", "0"):
+        for pre in ("1", "0"):
+            monkeypatch.setenv("ZK_D0T", d0t)
+            monkeypatch.setenv("ZK_PRELAUNCH", pre)
+            ctx = zk_amd.Context(0)
+            try:
+                assert _prove(ctx, field, n) == want, f"ZK_D0T={d0t} ZK_PRELAUNCH={pre}"
+            finally:
+                ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 2])
+@pytest.mark.parametrize("n", [23, 24])
+def test_three_round_first_pass_agrees_large(monkeypatch, field, n):
+    got = {}
+    for d0t in ("1", "0"):
+        monkeypatch.setenv("ZK_D0T", d0t)
+        ctx = zk_amd.Context(0)
+        try:
+            got[d0t] = _prove(ctx, field, n)
         finally:
             ctx.close()
     assert got["1"] == got["0"]

@@ -62,15 +62,21 @@ def _oracle(field: int, n: int) -> dict:
 def _steps(nloc: int, d0: bool = True) -> int:
     """Kernel steps of a phase of nloc rounds, one all-reduce each: round 0,
     round 1, one more single round if nloc - 2 is odd, then two rounds per step.
-    With ZK_D0 (default) an even phase runs rounds 0 and 1 in one step."""
+    With ZK_D0 (default) an even phase runs rounds 0 and 1 in one step; an odd
+    phase of >= 11 rounds runs rounds 0-2 in one step (ZK_D0T), then rounds
+    3-4 in one step, then two rounds per step."""
+    if d0 and nloc >= 14 and nloc % 2 == 0:  # rounds 0-2, 3-5, 6-7, then doubles
+        return 3 + (nloc - 8) // 2
     if d0 and nloc >= 2 and nloc % 2 == 0:
         return nloc // 2
+    if d0 and nloc >= 11:
+        return 2 + (nloc - 5) // 2
     if nloc <= 2:
         return nloc
     return 2 + (nloc - 2) % 2 + (nloc - 2) // 2
 
 
-@pytest.mark.parametrize("world,nloc,field", [(2, 12, 0), (4, 9, 2), (2, 0, 1), (2, 5, 0)])
+@pytest.mark.parametrize("world,nloc,field", [(2, 12, 0), (4, 9, 2), (2, 0, 1), (2, 5, 0), (2, 11, 1), (2, 14, 2)])
 def test_host_comm_ranks_match_single_process(tmp_path, world, nloc, field):
     res = _run(world, "host", field, nloc, str(tmp_path))
     want = _oracle(field, nloc + world.bit_length() - 1)

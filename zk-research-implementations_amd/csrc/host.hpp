@@ -204,6 +204,7 @@ struct zk_ctx {
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
   int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
+  bool d0t = true;          // odd variable counts (>= 11): rounds 0-2 in one pass, then fold by three (ZK_D0T)
   bool dm = true;           // double steps with two pending challenges on the matrix cores (k_gkr_dm; ZK_DM=0: k_gkr_dround)
   uint64_t dm_min_quads = 1u << 17;  // ... when they have at least this many quads (ZK_DM_MIN_QUADS; smaller steps are latency-bound: k_gkr_dround)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
@@ -400,8 +401,11 @@ inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks
   }
 }
 
+// product: the limb sums are sums of products of two Montgomery images (R^2
+// scale: REDC once); 17-word sums always are, 8-word sums are element sums
+// unless the kernel reduced product sums mod p in the block (k_gkr_d0t).
 template <class F, int K>
-void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
+void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K], bool product = false) {
   const bool multi = across_ranks && multi_rank(c);
   const int n = K * L;
   wait_flag(c, sk.tag);
@@ -413,7 +417,7 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
     if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
     c->stats.collectives += 1;
   }
-  for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w + L * k, L, L == 17);
+  for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w + L * k, L, L == 17 || product);
 }
 
 inline void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kSlotU64 * 8); }
@@ -525,7 +529,7 @@ struct GStep {
   int np;          // double / dtail: pending challenges at entry (1 or 2)
   uint32_t nd = 0; // dtail: double steps it runs
 };
-enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5 };
+enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5, GS_D0T = 6, GS_T32 = 7, GS_T33 = 8 };
 
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
@@ -535,12 +539,25 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   std::vector<GStep> steps;
   // rounds 0 and 1 in one pass over the inputs (default; same-box A/B at n = 24:
   // BN254 Fr 1.72-1.74 vs 1.82-1.85 ms, BLS12-381 Fr 1.76 vs 1.83 ms)
-  const bool d0 = c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
-  if (nv >= 1) steps.push_back({d0 ? GS_D0 : GS_ROUND0, 0, 0});
+  // rounds 0-2 in one pass over the inputs (k_gkr_d0t), the inputs folded by
+  // three at once: odd counts (>= 11) then run rounds 3-4 (k_gkr_dm3), even
+  // counts (>= 14) rounds 3-5 (k_gkr_t33) and, folding by three again, 6-7
+  // (k_gkr_dm3); double steps follow
+  const bool d0t = c->dround && c->d0t && ((nv >= 11 && nv % 2 == 1) || (nv >= 14 && nv % 2 == 0));
+  const bool d0 = !d0t && c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
+  if (nv >= 1) steps.push_back({d0t ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0), 0, 0});
+  uint32_t after_t = 5;
+  if (d0t && nv % 2 == 0) {
+    steps.push_back({GS_T33, 3, 3});
+    steps.push_back({GS_T32, 6, 3});
+    after_t = 8;
+  } else if (d0t) {
+    steps.push_back({GS_T32, 3, 3});
+  }
   if (c->dround) {
-    uint32_t i = d0 ? 2 : 1;
-    int np = d0 ? 2 : 1;  // challenges pending at the first double step
-    if (!d0) {
+    uint32_t i = d0t ? after_t : (d0 ? 2 : 1);
+    int np = d0t || d0 ? 2 : 1;  // challenges pending at the first double step
+    if (!d0 && !d0t) {
       if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
       if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
     }
@@ -585,7 +602,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
   std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
   int inbuf = -1;                        // work buffer holding cur (-1: the input tables)
-  Fe ra = zk::fe_zero<F>(), rb = zk::fe_zero<F>();  // last two challenges (non-pre-enqueued launches)
+  Fe rz = zk::fe_zero<F>(), ra = zk::fe_zero<F>(), rb = zk::fe_zero<F>();  // last three challenges (oldest first)
   auto out_tables = [&](uint64_t size, Fe* nx[4]) {
     const int ob = inbuf == 0 ? 1 : 0;
     Fe* w = c->work[ob].fe();
@@ -621,6 +638,48 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0r<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
       }
       enqueue_reduce(c, sk, across_ranks, zk::kD0Limbs);
+      return;
+    }
+    if (st.kind == GS_D0T) {  // rounds 0, 1, 2 over the input tables (size 8 O), nothing written
+      const uint64_t O = size / 8, nch = O / 32;
+      const uint32_t res = grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F>) & ~1u;
+      const uint32_t grid = (uint32_t)std::max<uint64_t>({res, 2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax)});
+      launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, sk);
+      enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
+      return;
+    }
+    if (st.kind == GS_T32 || st.kind == GS_T33) {  // fold level i-3 by three challenges to level i
+      const uint64_t Q = size / 4;
+      Fe* nx[4];
+      out_tables(size, nx);
+      zk::DIn din{};
+      if (pre) {
+        din.host = h_rpost(c);
+        din.relay = d_rpost(c);
+        din.err = h_err(c);
+        din.tag = rtags[si] = ++c->rtag;
+      } else {
+        din.ra = rz;
+        din.rb = ra;
+        din.rab = rb;  // carries r_{i-1} for this step
+      }
+      if (st.kind == GS_T33) {  // rounds i .. i+2 over level i's octants: 27 moment sums
+        const uint64_t O = size / 8, nch = O / 32;
+        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F>);
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax);
+        launch(c, ZK_K_GKR_DM, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
+               nx[1], nx[2], nx[3], O, din, sk);
+        for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+        enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
+        return;
+      }
+      const uint64_t nch = Q / zk::kDMQuads;
+      const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_dm3<F>);
+      const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
+      launch(c, ZK_K_GKR_DM, 4608.0 * Q, 48.0 * Q, zk::k_gkr_dm3<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
+             nx[1], nx[2], nx[3], Q, din, sk);
+      for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+      enqueue_reduce(c, sk, across_ranks, zk::kDLimbs);
       return;
     }
     if (st.kind == GS_TAIL) {
@@ -763,7 +822,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   auto hand_on = [&](size_t si) {
     if (!pre || si + 1 >= ns) return;
     const GStep& nx = steps[si + 1];
-    if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
+    if (nx.kind == GS_T32 || nx.kind == GS_T33) {
+      post.post2(rz, ra, rb, rtags[si + 1]);
+    } else if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
       if (nx.np == 2)
         post.post2(ra, rb, zk::hfe_mul<F>(ra, rb), rtags[si + 1]);
       else
@@ -774,8 +835,50 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   };
   auto one_round = [&](uint32_t i, const Fe& e0, const Fe& e1, const Fe& e2) {
     claim = finish_round<F>(tr, e0, e1, e2, k0 + i, out, r);
+    rz = ra;
     ra = rb;
     rb = r;
+  };
+  // rounds i0, i0 + 1, i0 + 2 from the 27 moment sums of k_gkr_d0t (tile id
+  // 9 alpha + 3 beta + gamma per axis: 0 = X0 Y0, 1 = X1 Y1, 2 = X0 Y1 + X1 Y0);
+  // X(t) Y(t) = (1-t)^2 m0 + t^2 m1 + t(1-t) ms, so at t = 2 the weights are (1, 4, -2)
+  auto three_rounds = [&](uint32_t i0, bool first) {
+    Fe T[zk::kD0TCats];
+    collect_sums<F, zk::kD0TCats>(c, sinks[i0], across_ranks, 8, T, true);
+    using namespace zk;
+    const Fe one = fe_one<F>(), two = hfe_add<F>(one, one), four = hfe_add<F>(two, two);
+    auto at2w = [&](const Fe& m0, const Fe& m1, const Fe& ms) {  // value at t = 2
+      return hfe_sub<F>(hfe_add<F>(m0, hfe_mul<F>(four, m1)), hfe_mul<F>(two, ms));
+    };
+    auto wts = [&](const Fe& t, Fe (&w)[3]) {
+      const Fe omt = hfe_sub<F>(one, t);
+      w[0] = hfe_mul<F>(omt, omt);
+      w[1] = hfe_mul<F>(t, t);
+      w[2] = hfe_mul<F>(t, omt);
+    };
+    Fe U[3];  // round i0: U[alpha] = sum over beta, gamma in {0, 1}
+    for (int a = 0; a < 3; ++a)
+      U[a] = hfe_add<F>(hfe_add<F>(T[9 * a], T[9 * a + 1]), hfe_add<F>(T[9 * a + 3], T[9 * a + 4]));
+    one_round(i0, U[0], first ? U[1] : hfe_sub<F>(claim, U[0]), at2w(U[0], U[1], U[2]));
+    Fe wa[3];
+    wts(r, wa);
+    Fe V[3];  // round i0 + 1: V[beta] = sum_alpha w(ra, alpha) sum_{gamma in {0, 1}}
+    for (int b = 0; b < 3; ++b) {
+      V[b] = fe_zero<F>();
+      for (int a = 0; a < 3; ++a)
+        V[b] = hfe_add<F>(V[b], hfe_mul<F>(wa[a], hfe_add<F>(T[9 * a + 3 * b], T[9 * a + 3 * b + 1])));
+    }
+    one_round(i0 + 1, V[0], hfe_sub<F>(claim, V[0]), at2w(V[0], V[1], V[2]));
+    Fe wb[3];
+    wts(r, wb);
+    Fe Z[3];  // round i0 + 2: Z[gamma] = sum w(ra, alpha) w(rb, beta) T
+    for (int g = 0; g < 3; ++g) {
+      Z[g] = fe_zero<F>();
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b)
+          Z[g] = hfe_add<F>(Z[g], hfe_mul<F>(hfe_mul<F>(wa[a], wb[b]), T[9 * a + 3 * b + g]));
+    }
+    one_round(i0 + 2, Z[0], hfe_sub<F>(claim, Z[0]), at2w(Z[0], Z[1], Z[2]));
   };
   // rounds i0 and i0 + 1 from a double step's eight product sums (the first
   // step of a phase, k_gkr_d0: nine, the ninth V11 for round 0's e1)
@@ -816,6 +919,15 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     } else if (st.kind == GS_D0) {
       two_rounds(0, true);
       pend = 2;
+    } else if (st.kind == GS_D0T) {
+      three_rounds(0, true);
+      pend = 3;
+    } else if (st.kind == GS_T32) {
+      two_rounds(st.i);
+      pend = 2;
+    } else if (st.kind == GS_T33) {
+      three_rounds(st.i, false);
+      pend = 3;
     } else if (st.kind == GS_SINGLE) {
       Fe s2[2];
       collect_sums<F, 2>(c, sinks[st.i], across_ranks, 17, s2);

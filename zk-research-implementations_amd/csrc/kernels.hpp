@@ -195,7 +195,7 @@ __device__ __forceinline__ Fe fold2c(const Fe& x00, const Fe& x01, const Fe& x10
 #define ZK_STAMP_AFTER(i, w) do { } while (0)
 #endif
 
-constexpr int kSlotU64 = 160;  // per-block partial slot: up to 160 limb sums (1280 B)
+constexpr int kSlotU64 = 256;  // per-block partial slot: up to 256 limb sums (2 KiB)
 
 struct RoundSink {
   uint64_t* partials;   // [gridDim.x + 8][kSlotU64]: one slot per block, then 8 shard slots

@@ -429,6 +429,53 @@ __device__ __forceinline__ void diag_to_words(const unsigned long long (&T)[64],
   }
 }
 
+// The eight grid-point values of the quad whose folded corners z[0..3] this
+// lane holds (wave w = table w) -> digit rows; barrier; wave w then runs the
+// products of pair w & 1 for categories 4 (w >> 1) .. +3 (two K = 32 MFMAs
+// each, K = the 64 quads of the chunk); barrier (the image is reused).
+template <class F>
+__device__ __forceinline__ void dm_products(const Fe (&z)[4], DMScratch& sc, i32x16 (&acc)[4]) {
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, pp = w & 1, cg = w >> 1;
+  const Fe v20 = at2<F>(z[0], z[2]), v21 = at2<F>(z[1], z[3]);  // reduced
+  dm_row<F>(sc.img[0][w][l], z[0]);
+  dm_row<F>(sc.img[2][w][l], z[1]);
+  dm_row<F>(sc.img[4][w][l], z[2]);
+  dm_row<F>(sc.img[3][w][l], kLazyDigits<F> ? lazy2(z[0], z[1]) : at2<F>(z[0], z[1]));
+  dm_row<F>(sc.img[7][w][l], kLazyDigits<F> ? lazy2(z[2], z[3]) : at2<F>(z[2], z[3]));
+  dm_row<F>(sc.img[5][w][l], v20);
+  dm_row<F>(sc.img[6][w][l], v21);
+  dm_row<F>(sc.img[1][w][l], kLazyDigits<F> ? lazy2(v20, v21) : at2<F>(v20, v21));
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t cat = 4 * cg + i;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const i32x4 fa = tr_frag(&sc.img[cat][2 * pp][32 * half][0]);
+      const i32x4 fb = tr_frag(&sc.img[cat][2 * pp + 1][32 * half][0]);
+      acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb, acc[i], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+}
+// tiles -> anti-diagonal sums -> 17 words per category -> grid limb sums
+template <class F>
+__device__ __forceinline__ void dm_epilogue(const i32x16 (&acc)[4], DMScratch& sc, const RoundSink& sink) {
+  const uint32_t t = threadIdx.x, l = t & 63, cg = t >> 7, col = l & 31, h = l >> 5;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      atomicAdd(&sc.T[4 * cg + i][row + col], (unsigned long long)(long long)acc[i][r]);
+    }
+  }
+  __syncthreads();
+  if (t < (uint32_t)kDCats) diag_to_words<F>(sc.T[t], sc.tot + t * 17);
+  __syncthreads();
+  grid_finish<kDLimbs>(sc, sink);
+}
+
 template <class F>
 __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                      const Fe* __restrict__ M, const Fe* __restrict__ P,
@@ -474,41 +521,362 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, 
       z[k] = dm_fold<F>(cur, wf);
       st_fold(X2, j + k * Q, z[k]);
     }
-    const Fe v20 = at2<F>(z[0], z[2]), v21 = at2<F>(z[1], z[3]);  // reduced
-    dm_row<F>(sc.img[0][w][l], z[0]);
-    dm_row<F>(sc.img[2][w][l], z[1]);
-    dm_row<F>(sc.img[4][w][l], z[2]);
-    dm_row<F>(sc.img[3][w][l], kLazyDigits<F> ? lazy2(z[0], z[1]) : at2<F>(z[0], z[1]));
-    dm_row<F>(sc.img[7][w][l], kLazyDigits<F> ? lazy2(z[2], z[3]) : at2<F>(z[2], z[3]));
-    dm_row<F>(sc.img[5][w][l], v20);
-    dm_row<F>(sc.img[6][w][l], v21);
-    dm_row<F>(sc.img[1][w][l], kLazyDigits<F> ? lazy2(v20, v21) : at2<F>(v20, v21));
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t cat = 4 * cg + i;
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const i32x4 fa = tr_frag(&sc.img[cat][2 * pp][32 * half][0]);
-        const i32x4 fb = tr_frag(&sc.img[cat][2 * pp + 1][32 * half][0]);
-        acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb, acc[i], 0, 0, 0);
-      }
-    }
-    __syncthreads();
+    dm_products<F>(z, sc, acc);
   }
-  const uint32_t col = l & 31, h = l >> 5;
+  dm_epilogue<F>(acc, sc, sink);
+}
+
+
+// ---------------------------------------------------------------------------
+// Rounds 0, 1 and 2 in one pass over the inputs (k_gkr_d0t, even schedules
+// start here: the first fold pass then writes 1/8 of the tables instead of
+// 1/4). An octant j < O holds the corners X_u = X[j + u O], u = 4a + 2b + c
+// (a = variable 0, the MSB). Along one variable X(t) Y(t) = (1-t)^2 X0 Y0 +
+// t(1-t) (X0 Y1 + X1 Y0) + t^2 X1 Y1, so the three rounds need, per axis, the
+// three "moments" 0 (X0 Y0), 1 (X1 Y1), s (X0 Y1 + X1 Y0): 27 moment tiles
+// T(alpha, beta, gamma) = sum_j sum of the 2^(#s) corner products X_u Y_v
+// they stand for — 64 corner-pair products per octant and product, all on
+// corner digits (no extended points, no VALU arithmetic beyond the digits).
+// The host (three_rounds) evaluates any grid point from the tiles with the
+// weights (1-t)^2, t^2, t(1-t). Block b serves product b & 1 (A*S or M*P);
+// per chunk of 32 octants wave w loads corners 2w and 2w+1 of both tables
+// (lanes 0-31 X, 32-63 Y) and writes their digit rows into a double-buffered
+// image [corner][table][32][32]; after one barrier wave w = 2 aX + aY runs the
+// 16 products X_u Y_v with u in aX's half (variable 0 = aX) and v in aY's:
+// their tiles share the variable-0 moment (aX == aY ? aX : s), so a wave
+// holds 9 tiles (b, c moments) and reads 8 fragments per chunk. The two s
+// waves add into the same tiles. Output: per tile the block's sum + p 2^275
+// as 17 words,
+// reduced mod p in the block (3 Montgomery multiplies): 27 x 8 limb sums.
+// ---------------------------------------------------------------------------
+constexpr int kD0TCats = 27;
+constexpr int kD0TLimbs = kD0TCats * 8;  // 216 limb sums (8-word reduced product sums)
+constexpr uint32_t kD0TChunksMax = 512;  // chunks per block: a tile slot takes <= 8 MFMAs (2^22) per chunk
+// moment digit of one axis: corners (x, y) -> 0, 1 or 2 (= s)
+__host__ __device__ constexpr int moment_digit(int x, int y) { return x == y ? x : 2; }
+
+// (x0 + x1 2^256 + x2 2^512) mod p for the 17-word block sum (Montgomery multiplies by R^2)
+template <class F>
+__device__ __forceinline__ Fe words17_mod_p(const uint64_t* w) {
+  Fe c0, c1, c2 = fe_zero<F>(), r2;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 8; ++i) {
+    c0.v[i] = (uint32_t)w[i];
+    c1.v[i] = (uint32_t)w[8 + i];
+    r2.v[i] = F::R2[i];
+  }
+  c2.v[0] = (uint32_t)w[16];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {  // 2^256 < 6p for the three fields
+    c0 = fe_reduce_once<F>(c0);
+    c1 = fe_reduce_once<F>(c1);
+  }
+  const Fe t1 = fe_mul<F>(c1, r2);                    // c1 R
+  const Fe t2 = fe_mul<F>(fe_mul<F>(c2, r2), r2);     // c2 R^2
+  return fe_add<F>(fe_add<F>(c0, t1), t2);
+}
+
+struct D0TScratch {
+  uint8_t img[2][8][2][32][32];  // buffer, corner, table (X, Y), octant, digit row (32 KiB)
+  unsigned long long T[kD0TCats][64];
+  uint64_t w17[kD0TCats][17];
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+};
+
+// wave w = 2 aX + aY: products X_u Y_v, u = 4 aX + ux, v = 4 aY + vy; tile slot 3 d_b + d_c
+__device__ __forceinline__ void d0t_mfmas(const uint8_t (*img)[2][32][32], i32x16 (&acc)[9]) {
+  const uint32_t w = threadIdx.x >> 6, aX = w >> 1, aY = w & 1;
+  i32x4 fa[4], fb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fa[k] = tr_frag(&img[4 * aX + k][0][0][0]);
+    fb[k] = tr_frag(&img[4 * aY + k][1][0][0]);
+  }
+#pragma unroll
+  for (int ux = 0; ux < 4; ++ux)
+#pragma unroll
+    for (int vy = 0; vy < 4; ++vy) {
+      const int slot = 3 * moment_digit(ux >> 1, vy >> 1) + moment_digit(ux & 1, vy & 1);
+      acc[slot] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ux], fb[vy], acc[slot], 0, 0, 0);
+    }
+}
+__device__ __forceinline__ void d0t_flush(const i32x16 (&acc)[9], unsigned long long (&T)[kD0TCats][64]) {
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63, col = l & 31, h = l >> 5;
+  const uint32_t da = (uint32_t)moment_digit((int)(w >> 1), (int)(w & 1));
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      atomicAdd(&sc.T[4 * cg + i][row + col], (unsigned long long)(long long)acc[i][r]);
+      atomicAdd(&T[9 * da + i][row + col], (unsigned long long)(long long)acc[i][r]);
+    }
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                      const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t O,
+                                                      RoundSink sink) {
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  __shared__ D0TScratch sc;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, half = l >> 5, ql = l & 31;
+  for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  i32x16 acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0;
+  const uint32_t pp = blockIdx.x & 1;
+  const Fe* __restrict__ T = half ? (pp ? P : S) : (pp ? M : A);
+  const uint64_t nch = O / 32, nb = gridDim.x >> 1;
+  uint64_t ch = blockIdx.x >> 1;
+  Fe cn[2];
+  if (ch < nch) {
+    cn[0] = ld_fe(T, ch * 32 + ql + (2 * w) * O);
+    cn[1] = ld_fe(T, ch * 32 + ql + (2 * w + 1) * O);
+  }
+  uint32_t buf = 0;
+  for (; ch < nch; ch += nb, buf ^= 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      to_digits(cn[i]);
+      st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
+    }
+    if (ch + nb < nch) {  // the next chunk's corners, in flight during this chunk's products
+      cn[0] = ld_fe(T, (ch + nb) * 32 + ql + (2 * w) * O);
+      cn[1] = ld_fe(T, (ch + nb) * 32 + ql + (2 * w + 1) * O);
+    }
+    __syncthreads();  // the image of this chunk is complete (double buffering: one barrier per chunk)
+    d0t_mfmas(sc.img[buf], acc);
+  }
+  __syncthreads();
+  d0t_flush(acc, sc.T);
+  __syncthreads();
+  if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
+  __syncthreads();
+  if (t < (uint32_t)kD0TCats) {
+    const Fe x = words17_mod_p<F>(sc.w17[t]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc.tot[t * 8 + i] = x.v[i];
+  }
+  __syncthreads();
+  grid_finish<kD0TLimbs>(sc, sink);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_gkr_dm3: the double step after k_gkr_d0t — THREE pending challenges
+// (ra, rb, rc) = (r_{i-3}, r_{i-2}, r_{i-1}). The level-(i-3) tables fold to
+// level i in one pass by the multilinear extension's own weights:
+//   Z[e] = sum_c eq((ra, rb, rc), c) X[e + c 4Q],  c = 4a + 2b + c0 (a: ra's variable),
+// (partial_evaluate three times, multilinear_polynomial_evaluation.rs:52-63), as ONE
+// K = 256 MFMA product per 32 elements: A = digits of w_c[k] = eq(r, c)
+// 2^(8k + 64) mod p, B = the inputs' own digits (every input is < p: no
+// differences, no lazy ranges). Then the eight grid-point products of
+// rounds i, i+1 over level i's quads, exactly as k_gkr_dm.
+// ---------------------------------------------------------------------------
+struct DM3Scratch : DMScratch {
+  Fe eqw[8];
+};
+template <class F>
+__device__ __forceinline__ Fe dm3_fold(Fe (&x)[8], const i32x4 (&wf)[8]) {
+  const bool h = (threadIdx.x & 32) != 0;
+  i32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    to_digits(x[c]);
+    i32x4 own_lo, own_hi, got;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      own_lo[q] = (int)x[c].v[q];
+      own_hi[q] = (int)x[c].v[4 + q];
+      got[q] = (int)xchg32(h ? x[c].v[q] : x[c].v[4 + q]);
+    }
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? got : own_lo, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? own_hi : got, acc1, 0, 0, 0);
+  }
+  int64_t W[8];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int64_t keep = h ? word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3])
+                           : word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
+    const int64_t send = h ? word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3])
+                           : word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
+    const uint32_t lo = xchg32((uint32_t)send), hi = xchg32((uint32_t)((uint64_t)send >> 32));
+    const int64_t recv = (int64_t)(((uint64_t)hi << 32) | lo);
+    W[2 * g] = h ? recv : keep;
+    W[2 * g + 1] = h ? keep : recv;
+  }
+  return dm_finish<F>(W, fe_zero<F>());
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock, 2) void k_gkr_dm3(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                      const Fe* __restrict__ M, const Fe* __restrict__ P,
+                                                      Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
+                                                      Fe* __restrict__ P2, uint64_t Q, DIn din, RoundSink sink) {
+  Fe ra, rb, rc;
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc (not ra rb) for this step
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
+  __shared__ DM3Scratch sc;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  if (t < 8) {  // eq((ra, rb, rc), c), c = 4a + 2b + c0
+    const Fe one = fe_one<F>();
+    const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
+    const Fe fc = (t & 1) ? rc : fe_sub<F>(one, rc);
+    sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
+  }
+  for (uint32_t i = t; i < kDCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  __syncthreads();
+  // the constants' digit rows borrow the product image until their fragments are in registers
+  uint8_t(*wimg)[32][32] = reinterpret_cast<uint8_t(*)[32][32]>(&sc.img[0][0][0][0]);
+  dm_row<F>(wimg[t >> 5][t & 31], fe_mul<F>(sc.eqw[t >> 5], p2dig<F>(t & 31)));
+  __syncthreads();
+  i32x4 wf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
+  __syncthreads();
+  const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
+  Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
+  i32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0;
+  const uint64_t nch = Q / kDMQuads, h4 = 4 * Q;
+  for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const uint64_t j = ch * kDMQuads + l;
+    Fe z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      Fe x[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) x[c] = ld_fe(X, j + k * Q + c * h4);
+      z[k] = dm3_fold<F>(x, wf);
+      st_fold(X2, j + k * Q, z[k]);
+    }
+    dm_products<F>(z, sc, acc);
+  }
+  dm_epilogue<F>(acc, sc, sink);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_gkr_t33: the step after k_gkr_d0t on even schedules — fold the inputs
+// (level i-3) by the three pending challenges to level i (k_gkr_dm3's K = 256
+// eq-weight MFMA) and sum rounds i, i+1, i+2 over level i's octants as 27
+// moment tiles (k_gkr_d0t's products, both pairs into the same tiles). Per
+// chunk of 32 octants wave w folds table w's 256 outputs in four 64-lane
+// calls (lane l: octant l & 31, corner 2f + (l >> 5)) and writes their digit
+// rows into a double-buffered image [corner][table][32][32]; after one
+// barrier wave w = 2 aX + aY runs 2 x 16 products into its 9 tiles. One
+// wave per SIMD (the tiles, the eight weight fragments and a fold's inputs
+// in flight: ~370 registers); the next fold's inputs are loaded before the
+// current one is reduced.
+// ---------------------------------------------------------------------------
+struct T33Scratch {
+  uint8_t img[2][8][4][32][32];  // buffer, corner, table, octant, digit row (64 KiB)
+  unsigned long long T[kD0TCats][64];
+  uint64_t w17[kD0TCats][17];
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+  Fe eqw[8];
+};
+
+template <class F>
+__global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                      const Fe* __restrict__ M, const Fe* __restrict__ P,
+                                                      Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
+                                                      Fe* __restrict__ P2, uint64_t O, DIn din, RoundSink sink) {
+  Fe ra, rb, rc;
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc for this step
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
+  __shared__ T33Scratch sc;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
+  if (t < 8) {  // eq((ra, rb, rc), c), c = 4a + 2b + c0
+    const Fe one = fe_one<F>();
+    const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
+    const Fe fc = (t & 1) ? rc : fe_sub<F>(one, rc);
+    sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
+  }
+  for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  __syncthreads();
+  uint8_t(*wimg)[32][32] = reinterpret_cast<uint8_t(*)[32][32]>(&sc.img[0][0][0][0][0]);
+  dm_row<F>(wimg[t >> 5][t & 31], fe_mul<F>(sc.eqw[t >> 5], p2dig<F>(t & 31)));
+  __syncthreads();
+  i32x4 wf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
+  __syncthreads();
+  const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
+  Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
+  i32x16 acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0;
+  const uint64_t nch = O / 32, h8 = 8 * O;  // level-i tables hold 8 O elements
+  auto in_at = [&](uint64_t ch, int f, Fe (&x)[8]) {
+    const uint64_t e = ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
+  };
+  Fe nx[8];
+  if ((uint64_t)blockIdx.x < nch) in_at(blockIdx.x, 0, nx);
+  uint32_t buf = 0;
+  for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x, buf ^= 1) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      Fe x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = nx[k];
+      if (f < 3)
+        in_at(ch, f + 1, nx);
+      else if (ch + gridDim.x < nch)
+        in_at(ch + gridDim.x, 0, nx);
+      const uint32_t corner = 2 * f + hh;
+      const Fe z = dm3_fold<F>(x, wf);
+      st_fold(X2, ch * 32 + ql + (uint64_t)corner * O, z);
+      dm_row<F>(sc.img[buf][corner][w][ql], z);
+    }
+    __syncthreads();  // this chunk's image is complete (double buffering: one barrier per chunk)
+    const uint32_t aX = w >> 1, aY = w & 1;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      i32x4 fa[4], fb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        fa[k] = tr_frag(&sc.img[buf][4 * aX + k][2 * pp][0][0]);
+        fb[k] = tr_frag(&sc.img[buf][4 * aY + k][2 * pp + 1][0][0]);
+      }
+#pragma unroll
+      for (int ux = 0; ux < 4; ++ux)
+#pragma unroll
+        for (int vy = 0; vy < 4; ++vy) {
+          const int slot = 3 * moment_digit(ux >> 1, vy >> 1) + moment_digit(ux & 1, vy & 1);
+          acc[slot] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ux], fb[vy], acc[slot], 0, 0, 0);
+        }
     }
   }
   __syncthreads();
-  if (t < (uint32_t)kDCats) diag_to_words<F>(sc.T[t], sc.tot + t * 17);
+  d0t_flush(acc, sc.T);
   __syncthreads();
-  grid_finish<kDLimbs>(sc, sink);
+  if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
+  __syncthreads();
+  if (t < (uint32_t)kD0TCats) {
+    const Fe x = words17_mod_p<F>(sc.w17[t]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc.tot[t * 8 + i] = x.v[i];
+  }
+  __syncthreads();
+  grid_finish<kD0TLimbs>(sc, sink);
 }
 
 }  // namespace zk
