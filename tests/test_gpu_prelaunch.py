@@ -234,23 +234,27 @@ def test_matrix_core_double_steps_agree_22var(monkeypatch, field):
 
 
 @pytest.mark.parametrize("field", [0, 1, 2])
-@pytest.mark.parametrize("n", [11, 13, 14, 15, 16, 18])
+@pytest.mark.parametrize("n", [11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
 def test_three_round_first_pass_matches_oracle(monkeypatch, field, n):
-    """Rounds 0-2 in one pass over the inputs (k_gkr_d0t: 27 moment tiles of
-    corner-pair products on the matrix cores), then the inputs folded by
-    (r0, r1, r2) at once (eq weights, K = 256): odd n >= 11 run rounds 3-4
-    there (k_gkr_dm3), even n >= 14 rounds 3-5 (k_gkr_t33: 27 moment tiles
-    over the folded octants) and fold by three once more for rounds 6-7
-    (k_gkr_dm3); double steps follow. ZK_D0T=0 keeps the two-round first
-    pass. Both give the oracle's proof, pre-enqueued and launched per step."""
+    """Three rounds per pass (host.hpp gkr_phase): rounds 0-2 over the inputs
+    (k_gkr_d0t: 27 moment tiles of corner-pair products on the matrix cores);
+    triple steps that fold by the three pending challenges (eq weights,
+    K = 256) and sum three rounds as 27 moment tiles (k_gkr_t33); one
+    two-round step folding by three (k_gkr_dm3); double steps. ZK_TTAIL=1:
+    triple steps to the end with 0-2 two-round steps (k_gkr_dm3, k_gkr_dm) so
+    the rest is a multiple of three (n = 11..20 cover all three cases), the
+    small ones in the persistent k_gkr_ttail (pre-enqueued) or one k_gkr_ttail
+    launch per step (ZK_PRELAUNCH=0). ZK_D0T=0 keeps the two-round schedule.
+    All give the oracle's proof."""
     want = _oracle(field, n)
-    for d0t in ("1", "0"):
+    for d0t, tt in (("1", "0"), ("1", "1"), ("0", "0")):
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_D0T", d0t)
+            monkeypatch.setenv("ZK_TTAIL", tt)
             monkeypatch.setenv("ZK_PRELAUNCH", pre)
             ctx = zk_amd.Context(0)
             try:
-                assert _prove(ctx, field, n) == want, f"ZK_D0T={d0t} ZK_PRELAUNCH={pre}"
+                assert _prove(ctx, field, n) == want, f"ZK_D0T={d0t} ZK_TTAIL={tt} ZK_PRELAUNCH={pre}"
             finally:
                 ctx.close()
 

@@ -62,15 +62,19 @@ def _oracle(field: int, n: int) -> dict:
 def _steps(nloc: int, d0: bool = True) -> int:
     """Kernel steps of a phase of nloc rounds, one all-reduce each: round 0,
     round 1, one more single round if nloc - 2 is odd, then two rounds per step.
-    With ZK_D0 (default) an even phase runs rounds 0 and 1 in one step; an odd
-    phase of >= 11 rounds runs rounds 0-2 in one step (ZK_D0T), then rounds
-    3-4 in one step, then two rounds per step."""
-    if d0 and nloc >= 14 and nloc % 2 == 0:  # rounds 0-2, 3-5, 6-7, then doubles
-        return 3 + (nloc - 8) // 2
+    With ZK_D0 (default) an even phase runs rounds 0 and 1 in one step; a phase
+    of >= 11 rounds (ZK_D0T) rounds 0-2, nt triple steps, one two-round step
+    folding by three, then two rounds per step."""
+    if d0 and nloc >= 11:  # three rounds per pass (host.hpp gkr_phase): d0t, nt triples, one fold-by-three double, doubles
+        nt, k = -1, 0
+        while 3 + 3 * k + 8 <= nloc:
+            r = nloc - 3 - 3 * k
+            if r % 2 == 0 and (r >= 12 or nt < 0):
+                nt = k
+            k += 1
+        return 1 + nt + 1 + (nloc - 5 - 3 * nt) // 2
     if d0 and nloc >= 2 and nloc % 2 == 0:
         return nloc // 2
-    if d0 and nloc >= 11:
-        return 2 + (nloc - 5) // 2
     if nloc <= 2:
         return nloc
     return 2 + (nloc - 2) % 2 + (nloc - 2) // 2

@@ -1,8 +1,9 @@
 """Print the kernels of the last proof in a rocprofv3 kernel trace (durations, gaps)."""
 import csv, glob, sys
-path = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
+path = sys.argv[1] if sys.argv[1].endswith(".csv") else glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "k_gkr_round0" in r["Kernel_Name"]]
+first = ("k_gkr_round0", "k_gkr_d0")  # the first step of a proof
+starts = [i for i, r in enumerate(rows) if any(f in r["Kernel_Name"] for f in first)]
 rows = rows[starts[-1]:]
 prev = None
 tot = 0.0

@@ -204,7 +204,8 @@ struct zk_ctx {
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
   int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
-  bool d0t = true;          // odd variable counts (>= 11): rounds 0-2 in one pass, then fold by three (ZK_D0T)
+  bool d0t = true;          // nv >= 11: rounds 0-2 in one pass, then steps that fold by three (ZK_D0T)
+  bool ttail = false;       // (d0t) triple steps to the end, the small ones in k_gkr_ttail (ZK_TTAIL; slower)
   bool dm = true;           // double steps with two pending challenges on the matrix cores (k_gkr_dm; ZK_DM=0: k_gkr_dround)
   uint64_t dm_min_quads = 1u << 17;  // ... when they have at least this many quads (ZK_DM_MIN_QUADS; smaller steps are latency-bound: k_gkr_dround)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
@@ -529,7 +530,11 @@ struct GStep {
   int np;          // double / dtail: pending challenges at entry (1 or 2)
   uint32_t nd = 0; // dtail: double steps it runs
 };
-enum { GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5, GS_D0T = 6, GS_T32 = 7, GS_T33 = 8 };
+enum {
+  GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5, GS_D0T = 6, GS_T32 = 7, GS_T33 = 8,
+  GS_TT = 9,     // one small triple step (k_gkr_ttail, one step per launch)
+  GS_TTAIL = 10  // the small triple steps in one persistent kernel (k_gkr_ttail)
+};
 
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
@@ -539,25 +544,62 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   std::vector<GStep> steps;
   // rounds 0 and 1 in one pass over the inputs (default; same-box A/B at n = 24:
   // BN254 Fr 1.72-1.74 vs 1.82-1.85 ms, BLS12-381 Fr 1.76 vs 1.83 ms)
-  // rounds 0-2 in one pass over the inputs (k_gkr_d0t), the inputs folded by
-  // three at once: odd counts (>= 11) then run rounds 3-4 (k_gkr_dm3), even
-  // counts (>= 14) rounds 3-5 (k_gkr_t33) and, folding by three again, 6-7
-  // (k_gkr_dm3); double steps follow
-  const bool d0t = c->dround && c->d0t && ((nv >= 11 && nv % 2 == 1) || (nv >= 14 && nv % 2 == 0));
-  const bool d0 = !d0t && c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
-  if (nv >= 1) steps.push_back({d0t ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0), 0, 0});
-  uint32_t after_t = 5;
-  if (d0t && nv % 2 == 0) {
-    steps.push_back({GS_T33, 3, 3});
-    steps.push_back({GS_T32, 6, 3});
-    after_t = 8;
-  } else if (d0t) {
-    steps.push_back({GS_T32, 3, 3});
+  // Three rounds per pass (ZK_D0T, nv >= 11): rounds 0-2 over the inputs
+  // (k_gkr_d0t), then nt triple steps that fold by the three pending
+  // challenges and run three rounds (k_gkr_t33), one two-round step that
+  // folds by three (k_gkr_dm3), and double steps (the small ones in the
+  // persistent k_gkr_dtail). nt: the largest count leaving an even number
+  // R >= 12 of rounds after the triples, else the smallest leaving an even
+  // R >= 8 (every matrix-core step needs >= 64 quads / 32 octants).
+  // ZK_TTAIL=1 (measured slower, kept for A/B): triple steps to the end, the
+  // small ones in the persistent k_gkr_ttail, with 0-2 two-round steps so the
+  // rest is a multiple of three. Its one-wave-per-SIMD MFMA steps are
+  // latency-bound on tiny levels (~45 us per triple step against ~11 us per
+  // double step of k_gkr_dtail).
+  const bool d0t = c->dround && c->d0t && nv >= 11;
+  int nt = -1;
+  if (d0t && !c->ttail)
+    for (int k = 0; 3 + 3 * k + 8 <= (int)nv; ++k) {
+      const int R = (int)nv - 3 - 3 * k;
+      if (R % 2 == 0 && (R >= 12 || nt < 0)) nt = k;
+    }
+  const bool d0t_doubles = d0t && !c->ttail && nt >= 0;
+  const bool d0t_triples = d0t && c->ttail;
+  const bool d0 = !d0t_doubles && !d0t_triples && c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
+  if (nv >= 1) steps.push_back({d0t_doubles || d0t_triples ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0), 0, 0});
+  if (d0t_doubles) {
+    for (int k = 0; k < nt; ++k) steps.push_back({GS_T33, 3u + 3u * k, 3});
+    steps.push_back({GS_T32, 3u + 3u * nt, 3});
   }
-  if (c->dround) {
-    uint32_t i = d0t ? after_t : (d0 ? 2 : 1);
-    int np = d0t || d0 ? 2 : 1;  // challenges pending at the first double step
-    if (!d0 && !d0t) {
+  if (d0t_triples) {
+    const int R = (int)nv - 3;
+    int a = 0;
+    while ((R - 2 * a) % 3 != 0) ++a;
+    int ntri = (R - 2 * a) / 3;
+    uint32_t i = 3;
+    while (ntri > 0 && (int)nv - (int)i >= 16) {
+      steps.push_back({GS_T33, i, 3});
+      i += 3;
+      --ntri;
+    }
+    for (int k = 0; k < a; ++k, i += 2) steps.push_back({k == 0 ? GS_T32 : GS_DOUBLE, i, k == 0 ? 3 : 2});
+    const int np0 = a > 0 ? 2 : 3;
+    if (ntri > 0 && pre && c->dtail && use_tail(c, across_ranks) && ntri <= 64) {
+      steps.push_back({GS_TTAIL, i, np0, (uint32_t)ntri});
+      const uint64_t O0 = (L >> i) / 8;
+      const size_t had = c->tailbuf.bytes;
+      c->tailbuf.ensure(kTailRelayBytes + zk::ttail_region(O0, (uint32_t)ntri) * sizeof(Fe));
+      if (c->tailbuf.bytes != had) HIPCK(hipMemset(c->tailbuf.p, 0, kTailRelayBytes));  // relay tags at rest
+    } else {
+      for (int k = 0; k < ntri; ++k, i += 3) steps.push_back({GS_TT, i, k == 0 ? np0 : 3});
+    }
+  }
+  if (d0t_triples) {
+    // (the schedule above covers every round)
+  } else if (c->dround) {
+    uint32_t i = d0t_doubles ? 5u + 3u * nt : (d0 ? 2 : 1);
+    int np = d0t_doubles || d0 ? 2 : 1;  // challenges pending at the first double step
+    if (!d0 && !d0t_doubles) {
       if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
       if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
     }
@@ -599,6 +641,23 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
   }
   const size_t ns = steps.size();
+  {  // the schedule covers rounds 0 .. nv-1 exactly once, in order (checked before anything launches)
+    uint32_t next = 0;
+    for (const GStep& st : steps) {
+      uint32_t nr = 1;
+      switch (st.kind) {
+        case GS_DOUBLE: case GS_D0: case GS_T32: nr = 2; break;
+        case GS_D0T: case GS_T33: case GS_TT: nr = 3; break;
+        case GS_DTAIL: nr = 2 * st.nd; break;
+        case GS_TTAIL: nr = 3 * st.nd; break;
+        case GS_TAIL: nr = nv - st.i; break;
+        default: nr = 1;
+      }
+      if (st.i != next) fail(ZK_EINVAL, "internal: step schedule out of order");
+      next += nr;
+    }
+    if (next != nv) fail(ZK_EINVAL, "internal: step schedule does not cover every round");
+  }
   std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
   std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
   int inbuf = -1;                        // work buffer holding cur (-1: the input tables)
@@ -646,6 +705,54 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       const uint32_t grid = (uint32_t)std::max<uint64_t>({res, 2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax)});
       launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
+      return;
+    }
+    if (st.kind == GS_TT || st.kind == GS_TTAIL) {  // small triple steps (k_gkr_ttail)
+      const uint64_t O0 = size / 8;
+      const uint32_t nd = st.kind == GS_TTAIL ? st.nd : 1u;
+      zk::TTailArgs a{};
+      for (int t = 0; t < 4; ++t) a.in[t] = cur[t];
+      a.O0 = O0;
+      a.nsteps = nd;
+      a.np0 = (uint32_t)st.np;
+      a.err = h_err(c);
+      uint32_t grid;
+      if (st.kind == GS_TTAIL) {
+        for (uint32_t d = 1; d < nd; ++d) sinks[i + 3 * d] = make_sink(c, across_ranks);
+        a.relay = reinterpret_cast<zk::RPost*>(c->tailbuf.p);
+        a.out = reinterpret_cast<Fe*>(reinterpret_cast<char*>(c->tailbuf.p) + kTailRelayBytes);
+        a.host = h_rpost(c);
+        rtags[si] = c->rtag + 1;
+        c->rtag += nd;
+        a.rtag0 = rtags[si];
+        if (c->tail_trace) a.trace = c->tail_trace;
+        grid = (uint32_t)std::min<uint64_t>((uint64_t)c->num_cus, (O0 + 31) / 32);  // one block per CU: co-resident
+      } else {
+        Fe* nx[4];
+        out_tables(size, nx);
+        a.out = nx[0];  // 4 tables of 8 O0 back to back
+        a.relay = d_rpost(c);
+        if (pre) {
+          a.host = h_rpost(c);
+          a.rtag0 = rtags[si] = ++c->rtag;
+        } else {
+          a.r[0] = rz;
+          a.r[1] = ra;
+          a.r[2] = rb;
+        }
+        grid = (uint32_t)std::min<uint64_t>((uint64_t)c->num_cus, (O0 + 31) / 32);
+      }
+      double bytes = 0, muls = 0;
+      for (uint32_t d = 0; d < nd; ++d) {
+        const double O = (double)(O0 >> (3 * d)), nw = d == 0 ? (double)(1u << st.np) : 8.0;
+        bytes += (nw * 8 + 8) * 4 * 32 * O;
+        muls += 96.0 * O;
+      }
+      launch(c, ZK_K_GKR_DTAIL, bytes, muls, zk::k_gkr_ttail<F>, grid, a, sk);
+      const uint64_t Ol = O0 >> (3 * (nd - 1));
+      Fe* last = a.out + zk::ttail_region(O0, nd - 1);
+      for (int t = 0; t < 4; ++t) cur[t] = last + (uint64_t)t * 8 * Ol;
+      if (st.kind == GS_TT) enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
     }
     if (st.kind == GS_T32 || st.kind == GS_T33) {  // fold level i-3 by three challenges to level i
@@ -804,7 +911,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   // the highest challenge tag step si (and every step before it) waits for
   auto last_tag = [&](size_t si) {
     if (steps[si].kind == GS_TAIL) return rtags[si] + (nv - steps[si].i) - 1;
-    if (steps[si].kind == GS_DTAIL) return rtags[si] + steps[si].nd - 1;
+    if (steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL) return rtags[si] + steps[si].nd - 1;
     return rtags[si];
   };
   PostR post{c};
@@ -822,7 +929,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   auto hand_on = [&](size_t si) {
     if (!pre || si + 1 >= ns) return;
     const GStep& nx = steps[si + 1];
-    if (nx.kind == GS_T32 || nx.kind == GS_T33) {
+    if (nx.kind == GS_T32 || nx.kind == GS_T33 || nx.kind == GS_TT || nx.kind == GS_TTAIL) {
       post.post2(rz, ra, rb, rtags[si + 1]);
     } else if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
       if (nx.np == 2)
@@ -844,7 +951,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   // X(t) Y(t) = (1-t)^2 m0 + t^2 m1 + t(1-t) ms, so at t = 2 the weights are (1, 4, -2)
   auto three_rounds = [&](uint32_t i0, bool first) {
     Fe T[zk::kD0TCats];
-    collect_sums<F, zk::kD0TCats>(c, sinks[i0], across_ranks, 8, T, true);
+    collect_sums<F, zk::kD0TCats>(c, sinks[i0], across_ranks, 9, T, true);
     using namespace zk;
     const Fe one = fe_one<F>(), two = hfe_add<F>(one, one), four = hfe_add<F>(two, two);
     auto at2w = [&](const Fe& m0, const Fe& m1, const Fe& ms) {  // value at t = 2
@@ -925,8 +1032,14 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     } else if (st.kind == GS_T32) {
       two_rounds(st.i);
       pend = 2;
-    } else if (st.kind == GS_T33) {
+    } else if (st.kind == GS_T33 || st.kind == GS_TT) {
       three_rounds(st.i, false);
+      pend = 3;
+    } else if (st.kind == GS_TTAIL) {
+      for (uint32_t d = 0; d < st.nd; ++d) {
+        three_rounds(st.i + 3 * d, false);
+        if (d + 1 < st.nd) post.post2(rz, ra, rb, rtags[si] + d + 1);
+      }
       pend = 3;
     } else if (st.kind == GS_SINGLE) {
       Fe s2[2];
@@ -959,7 +1072,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint64_t* T = c->tail_trace + 512;
     uint64_t prev_pub = 0;
     for (size_t si = 0; si < ns; ++si) {
-      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL) break;
+      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
       const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0;  // no challenge to wait for
       fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f\n", si,
@@ -976,6 +1089,16 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       fprintf(stderr, "zk tail round %2u: wait r %6.2f us, fold+eval %6.2f, fan-in %6.2f, publish %6.2f, hand-off to next r %6.2f\n",
               m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
               (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, m + 1 < nr ? (T[m * 8 + 9] - T[m * 8 + 4]) * 0.01 : 0.0);
+  }
+  if (c->tail_trace && !steps.empty() && steps.back().kind == GS_TTAIL) {  // ZK_DEBUG_TAIL
+    HIPCK(hipStreamSynchronize(c->stream));
+    const uint64_t* T = c->tail_trace;
+    const uint32_t nd = steps.back().nd;
+    for (uint32_t m = 0; m < nd; ++m)
+      fprintf(stderr, "zk ttail step %u: wait r %6.2f us, constants %6.2f, fold+products %6.2f, epilogue %6.2f, fan-in+publish %6.2f, hand-off to next r %6.2f\n",
+              m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
+              (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, (T[m * 8 + 5] - T[m * 8 + 4]) * 0.01,
+              m + 1 < nd ? (T[m * 8 + 9] - T[m * 8 + 5]) * 0.01 : 0.0);
   }
   if (c->tail_trace && !steps.empty() && steps.back().kind == GS_DTAIL) {  // ZK_DEBUG_TAIL
     HIPCK(hipStreamSynchronize(c->stream));
@@ -1019,11 +1142,14 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   // each rank fills only its own slot of a zeroed limb-split vector.
   Fe* send = reinterpret_cast<Fe*>(d_gather(c) + 65536);  // 4 elements, after the bounce buffer
   if (nloc > 0) {
-    if (pend == 2) {  // the phase ended on a double round: cur has 4 elements per table, r_{nloc-2} pending too
-      Fe* t2 = send + 4;  // 4 x 2 scratch elements (the staging area below is written after a sync)
-      launch(c, ZK_K_FOLD, 8 * 96.0, 8.0, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], t2, t2 + 2, t2 + 4,
-             t2 + 6, (uint64_t)2, out.challenges[nloc - 2]);
-      for (int t = 0; t < 4; ++t) cur[t] = t2 + 2 * t;
+    // the phase ended with pend challenges not applied (cur: 2^pend elements per
+    // table): fold by r_{nloc-pend} .. r_{nloc-2} here, by r below
+    for (uint32_t k = pend; k > 1; --k) {
+      const uint64_t h = (uint64_t)1 << (k - 1);
+      Fe* t2 = send + 4 + (k == 3 ? 0 : 16);  // scratch (the staging area below is written after a sync)
+      launch(c, ZK_K_FOLD, 8 * h * 96.0, 8.0 * h, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], t2, t2 + h,
+             t2 + 2 * h, t2 + 3 * h, h, out.challenges[nloc - k]);
+      for (int t = 0; t < 4; ++t) cur[t] = t2 + h * t;
     }
     Fe* s4[4] = {send, send + 1, send + 2, send + 3};
     launch(c, ZK_K_FOLD, 4 * 96.0, 4.0, zk::k_fold4<F>, 1u, cur[0], cur[1], cur[2], cur[3], s4[0], s4[1], s4[2],

@@ -392,10 +392,12 @@ __device__ __forceinline__ void sum_slots(uint64_t* slots, uint32_t first, uint3
 constexpr uint32_t kAtomicFaninMax = 64;  // grids up to this size fan in through u64 atomics
 
 // Block limb sums are in sc.tot[0..C) (valid for threads < C); finish over the grid.
+// G: the blocks taking part (blocks 0 .. G-1; default the whole grid).
 template <int C, class Sc>
-__device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk) {
+__device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk, uint32_t G = 0) {
   static_assert(C <= kSlotU64 && C <= kBlock, "limb vector too long");
-  const uint32_t G = gridDim.x, t = threadIdx.x;
+  if (G == 0) G = gridDim.x;
+  const uint32_t t = threadIdx.x;
   if (G == 1) {
     ZK_STAMP(4);
     ZK_STAMP(5);

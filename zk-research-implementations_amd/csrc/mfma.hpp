@@ -550,30 +550,46 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, 
 // reduced mod p in the block (3 Montgomery multiplies): 27 x 8 limb sums.
 // ---------------------------------------------------------------------------
 constexpr int kD0TCats = 27;
-constexpr int kD0TLimbs = kD0TCats * 8;  // 216 limb sums (8-word reduced product sums)
+constexpr int kD0TLimbs = kD0TCats * 9;  // 243 limb sums (9 words per category, congruent mod p)
 constexpr uint32_t kD0TChunksMax = 512;  // chunks per block: a tile slot takes <= 8 MFMAs (2^22) per chunk
 // moment digit of one axis: corners (x, y) -> 0, 1 or 2 (= s)
 __host__ __device__ constexpr int moment_digit(int x, int y) { return x == y ? x : 2; }
 
-// (x0 + x1 2^256 + x2 2^512) mod p for the 17-word block sum (Montgomery multiplies by R^2)
+// A block's 17-word sum x (non-negative, normalised) -> 9 limb sums of a value
+// congruent to it mod p: words 0..7 plus sum_{w >= 8} x_w (2^(32 w) mod p),
+// each 32 x 32-bit product split over two columns (column sums < 2^37). The
+// host's hlimbs_to_fe takes any limb sums; 27 x 9 = 243 fit one slot.
+#define ZK_P2W_INIT(F)                                                                                          \
+  {pow2_mod_p<F>(256), pow2_mod_p<F>(288), pow2_mod_p<F>(320), pow2_mod_p<F>(352), pow2_mod_p<F>(384),             \
+   pow2_mod_p<F>(416), pow2_mod_p<F>(448), pow2_mod_p<F>(480), pow2_mod_p<F>(512)}
+static __constant__ Fe kP2WBn254Fr[9] = ZK_P2W_INIT(Bn254Fr);
+static __constant__ Fe kP2WBn254Fq[9] = ZK_P2W_INIT(Bn254Fq);
+static __constant__ Fe kP2WBls12_381Fr[9] = ZK_P2W_INIT(Bls12_381Fr);
 template <class F>
-__device__ __forceinline__ Fe words17_mod_p(const uint64_t* w) {
-  Fe c0, c1, c2 = fe_zero<F>(), r2;
+__device__ __forceinline__ Fe p2w(uint32_t k) {  // 2^(32 (8 + k)) mod p
+  if constexpr (F::id == BN254_FR) return kP2WBn254Fr[k];
+  else if constexpr (F::id == BN254_FQ) return kP2WBn254Fq[k];
+  else return kP2WBls12_381Fr[k];
+}
+template <class F>
+__device__ __forceinline__ void words17_to_limbs9(const uint64_t* x, uint64_t* out) {
+  uint64_t col[9];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c0.v[i] = (uint32_t)w[i];
-    c1.v[i] = (uint32_t)w[8 + i];
-    r2.v[i] = F::R2[i];
-  }
-  c2.v[0] = (uint32_t)w[16];
+  for (int j = 0; j < 8; ++j) col[j] = x[j];
+  col[8] = 0;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {  // 2^256 < 6p for the three fields
-    c0 = fe_reduce_once<F>(c0);
-    c1 = fe_reduce_once<F>(c1);
+  for (int w = 8; w < 17; ++w) {
+    const Fe k = p2w<F>(w - 8);
+    const uint32_t xw = (uint32_t)x[w];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t pr = (uint64_t)xw * k.v[j];
+      col[j] += (uint32_t)pr;
+      col[j + 1] += pr >> 32;
+    }
   }
-  const Fe t1 = fe_mul<F>(c1, r2);                    // c1 R
-  const Fe t2 = fe_mul<F>(fe_mul<F>(c2, r2), r2);     // c2 R^2
-  return fe_add<F>(fe_add<F>(c0, t1), t2);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) out[j] = col[j];
 }
 
 struct D0TScratch {
@@ -656,11 +672,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   __syncthreads();
   if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
   __syncthreads();
-  if (t < (uint32_t)kD0TCats) {
-    const Fe x = words17_mod_p<F>(sc.w17[t]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sc.tot[t * 8 + i] = x.v[i];
-  }
+  if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
   __syncthreads();
   grid_finish<kD0TLimbs>(sc, sink);
 }
@@ -680,14 +692,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
 struct DM3Scratch : DMScratch {
   Fe eqw[8];
 };
-template <class F>
-__device__ __forceinline__ Fe dm3_fold(Fe (&x)[8], const i32x4 (&wf)[8]) {
+template <class F, int NP = 3>
+__device__ __forceinline__ Fe dm3_fold(Fe (&x)[1 << NP], const i32x4 (&wf)[1 << NP]) {
   const bool h = (threadIdx.x & 32) != 0;
   i32x16 acc0, acc1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
+  for (int c = 0; c < (1 << NP); ++c) {
     to_digits(x[c]);
     i32x4 own_lo, own_hi, got;
 #pragma unroll
@@ -828,19 +840,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
   };
-  Fe nx[8];
-  if ((uint64_t)blockIdx.x < nch) in_at(blockIdx.x, 0, nx);
+  // inputs two folds ahead (one wave per SIMD: the loads in flight are what hides HBM latency)
+  Fe nx[8], nx2[8];
+  if ((uint64_t)blockIdx.x < nch) {
+    in_at(blockIdx.x, 0, nx);
+    in_at(blockIdx.x, 1, nx2);
+  }
   uint32_t buf = 0;
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x, buf ^= 1) {
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       Fe x[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = nx[k];
-      if (f < 3)
-        in_at(ch, f + 1, nx);
+      for (int k = 0; k < 8; ++k) {
+        x[k] = nx[k];
+        nx[k] = nx2[k];
+      }
+      if (f < 2)
+        in_at(ch, f + 2, nx2);
       else if (ch + gridDim.x < nch)
-        in_at(ch + gridDim.x, 0, nx);
+        in_at(ch + gridDim.x, f - 2, nx2);
       const uint32_t corner = 2 * f + hh;
       const Fe z = dm3_fold<F>(x, wf);
       st_fold(X2, ch * 32 + ql + (uint64_t)corner * O, z);
@@ -870,13 +889,174 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   __syncthreads();
   if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
   __syncthreads();
-  if (t < (uint32_t)kD0TCats) {
-    const Fe x = words17_mod_p<F>(sc.w17[t]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sc.tot[t * 8 + i] = x.v[i];
-  }
+  if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
   __syncthreads();
   grid_finish<kD0TLimbs>(sc, sink);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_gkr_ttail: the small triple steps of a proof in ONE persistent kernel
+// (one block per CU, all co-resident). Step s is a k_gkr_t33 step over
+// O0 >> 3s octants: fold by the pending challenges (step 0: np0 = 2 or 3,
+// then 3) and sum three rounds as 27 moment tiles. No launch sits between
+// steps (each kernel boundary costs ~10 us on the box); per step block 0
+// waits for the host's challenges (three self-tagged groups, tag rtag0 + s:
+// r_{i-3}, r_{i-2}, r_{i-1}; a two-challenge fold uses the last two) and
+// relays them through a fresh slot, min(grid, chunks) blocks fold and
+// multiply, and grid_finish over those blocks publishes (sink tag tag0 + s).
+// Tables written in step s are read by other blocks in step s+1: every store
+// and load of them is an 8-byte agent-scope atomic (sc1), every storing wave
+// drains before its block counts in, each step writes a fresh region
+// (MI355X_MICROARCH.md "Valid forms"), as k_gkr_dtail (step 0's inputs, from
+// the previous kernel, are read the same way). Octants past O (O < 32) are
+// zero lanes: every lane stays active for the transposed reads.
+// ---------------------------------------------------------------------------
+struct TTailArgs {
+  const Fe* in[4];    // step 0 inputs: 2^np0 * 8 O0 elements per table (level i0 - np0)
+  Fe* out;            // step s writes 4 tables of 8 (O0 >> 3s) at out + ttail_region(O0, s)
+  uint64_t O0;        // octants of step 0's level
+  uint32_t nsteps;
+  uint32_t np0;       // pending challenges at step 0 (2 or 3)
+  uint32_t rtag0;     // challenge tag awaited by step 0
+  const RPost* host;  // pinned challenge words
+  RPost* relay;       // nsteps fresh relay slots
+  uint32_t* err;      // pinned error word
+  Fe r[3];            // the challenges when host == null (one step launched after them)
+  uint64_t* trace;    // debug (ZK_DEBUG_TAIL): per step 8 s_memrealtime stamps of block 0, or null
+};
+#define ZK_TT_STAMP(tr, st, k) \
+  do { if ((tr) && blockIdx.x == 0 && threadIdx.x == 0) (tr)[(st) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__host__ __device__ __forceinline__ uint64_t ttail_region(uint64_t O0, uint32_t s) {
+  uint64_t o = 0;
+  for (uint32_t t = 0; t < s; ++t) o += 32 * (O0 >> (3 * t));
+  return o;
+}
+struct TTScratch {
+  uint8_t img[2][8][4][32][32];  // buffer, corner, table, octant, digit row (64 KiB)
+  unsigned long long T[kD0TCats][64];
+  uint64_t w17[kD0TCats][17];
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+  Fe eqw[8];
+};
+
+// one step of k_gkr_ttail with np pending challenges r[3 - np .. 2]; the block is
+// active. np = 2 runs as the three-challenge fold with the weights of inputs
+// 4..7 zero (and those inputs not loaded): one code path.
+template <class F>
+__device__ __forceinline__ void ttail_step(TTScratch& sc, const Fe (&r)[3], uint32_t np, const Fe* __restrict__ X,
+                                           Fe* __restrict__ X2, uint64_t O, uint32_t nb, const RoundSink& sk,
+                                           uint64_t* trace, uint32_t st) {
+  constexpr int NP = 3, NW = 8;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
+  const uint32_t nw = 1u << np;  // inputs per output
+  if (t < (uint32_t)NW) {  // eq((r_{3-np}, ..., r_2), c) for c < 2^np, else 0
+    const Fe one = fe_one<F>();
+    Fe e = one;
+    for (uint32_t b = 0; b < np; ++b) {
+      const Fe& rb = r[3 - np + b];
+      const bool bit = (t >> (np - 1 - b)) & 1;
+      e = fe_mul<F>(e, bit ? rb : fe_sub<F>(one, rb));
+    }
+    sc.eqw[t] = t < nw ? e : fe_zero<F>();
+  }
+  for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  __syncthreads();
+  uint8_t(*wimg)[32][32] = reinterpret_cast<uint8_t(*)[32][32]>(&sc.img[0][0][0][0][0]);
+  dm_row<F>(wimg[t >> 5][t & 31], fe_mul<F>(sc.eqw[t >> 5], p2dig<F>(t & 31)));
+  __syncthreads();
+  i32x4 wf[NW];
+#pragma unroll
+  for (int c = 0; c < NW; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
+  __syncthreads();
+  ZK_TT_STAMP(trace, st, 2);
+  i32x16 acc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[i][q] = 0;
+  const uint64_t nch = (O + 31) / 32, h8 = 8 * O;
+  uint32_t buf = 0;
+  for (uint64_t ch = blockIdx.x; ch < nch; ch += nb, buf ^= 1) {
+    const uint64_t j = ch * 32 + ql;
+    const bool valid = j < O;
+    for (int f = 0; f < 4; ++f) {  // not unrolled: one fold's inputs live at a time
+      const uint64_t e = j + (uint64_t)(2 * f + hh) * O;
+      Fe x[NW];
+#pragma unroll
+      for (int k = 0; k < NW; ++k) x[k] = valid && (uint32_t)k < nw ? ld_fe_a(X, e + k * h8) : fe_zero<F>();
+      Fe z = dm3_fold<F, NP>(x, wf);
+      if (valid) st_fe_a(X2, e, z);
+      else z = fe_zero<F>();
+      dm_row<F>(sc.img[buf][2 * f + hh][w][ql], z);
+    }
+    __syncthreads();
+    const uint32_t aX = w >> 1, aY = w & 1;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      i32x4 fa[4], fb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        fa[k] = tr_frag(&sc.img[buf][4 * aX + k][2 * pp][0][0]);
+        fb[k] = tr_frag(&sc.img[buf][4 * aY + k][2 * pp + 1][0][0]);
+      }
+#pragma unroll
+      for (int ux = 0; ux < 4; ++ux)
+#pragma unroll
+        for (int vy = 0; vy < 4; ++vy) {
+          const int slot = 3 * moment_digit(ux >> 1, vy >> 1) + moment_digit(ux & 1, vy & 1);
+          acc[slot] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ux], fb[vy], acc[slot], 0, 0, 0);
+        }
+    }
+  }
+  __syncthreads();
+  ZK_TT_STAMP(trace, st, 3);
+  d0t_flush(acc, sc.T);
+  __syncthreads();
+  if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
+  __syncthreads();
+  if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
+  __syncthreads();
+  ZK_TT_STAMP(trace, st, 4);
+  grid_finish<kD0TLimbs>(sc, sk, nb);  // drains every wave's table stores before its block counts in
+  ZK_TT_STAMP(trace, st, 5);
+  __syncthreads();                     // the scratch is reused next step
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock, 1) void k_gkr_ttail(TTailArgs a, RoundSink sink) {
+  __shared__ TTScratch sc;
+  for (uint32_t st = 0; st < a.nsteps; ++st) {
+    const uint64_t O = a.O0 >> (3 * st), nch = (O + 31) / 32;
+    const uint32_t nb = nch < gridDim.x ? (uint32_t)nch : gridDim.x;
+    if (blockIdx.x >= nb) return;  // idle from here on (nb never grows)
+    DIn din{};
+    din.ra = a.r[0];
+    din.rb = a.r[1];
+    din.rab = a.r[2];
+    din.host = a.host;
+    din.relay = a.relay + st;
+    din.err = a.err;
+    din.tag = a.rtag0 + st;
+    Fe r[3];
+    ZK_TT_STAMP(a.trace, st, 0);
+    block_get_rs(din, r[0], r[1], r[2], nb > 1);
+    ZK_TT_STAMP(a.trace, st, 1);
+    const uint32_t w = threadIdx.x >> 6;
+    const Fe* X;
+    if (st == 0) {
+      X = a.in[w];
+    } else {
+      const Fe* prev = a.out + ttail_region(a.O0, st - 1);  // 4 tables of 64 O
+      X = prev + (uint64_t)w * 64 * O;
+    }
+    Fe* X2 = a.out + ttail_region(a.O0, st) + (uint64_t)w * 8 * O;  // 4 tables of 8 O
+    RoundSink sk = sink;
+    sk.tag = sink.tag + st;
+    ttail_step<F>(sc, r, st == 0 ? a.np0 : 3u, X, X2, O, nb, sk, a.trace, st);
+  }
 }
 
 }  // namespace zk

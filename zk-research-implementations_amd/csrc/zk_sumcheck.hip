@@ -49,6 +49,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_DTAIL")) c->dtail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DM")) c->dm = atoi(e) != 0;
     if (const char* e = getenv("ZK_D0T")) c->d0t = atoi(e) != 0;
+    if (const char* e = getenv("ZK_TTAIL")) c->ttail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DM_MIN_QUADS")) c->dm_min_quads = strtoull(e, nullptr, 0);
     if (const char* e = getenv("ZK_D0")) c->d0 = atoi(e);
     if (const char* e = getenv("ZK_CIRCUIT_DENSE")) c->circuit_dense = atoi(e) != 0;
