@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 10u
+#define ZK_ABI_VERSION 11u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -82,8 +82,9 @@ enum {
   ZK_K_GKR_DROUND = 11, /* two rounds per kernel: pending folds + round sums + next round's quadratics (k_gkr_dround) */
   ZK_K_GKR_DTAIL = 12, /* the small double rounds in one persistent kernel (k_gkr_dtail) */
   ZK_K_GKR_D0 = 13,    /* rounds 0 and 1 in one pass over the input tables (k_gkr_d0m on the matrix cores; k_gkr_d0r / k_gkr_d0) */
-  ZK_K_GKR_DM = 14,    /* double steps with two pending challenges on the matrix cores (k_gkr_dm) */
-  ZK_K_KINDS = 15
+  ZK_K_GKR_DM = 14,    /* two-round steps on the matrix cores that fold by two or three challenges (k_gkr_dm, k_gkr_dm3) */
+  ZK_K_GKR_T33 = 15,   /* three-round steps on the matrix cores: fold by three + 27 moment sums (k_gkr_t33) */
+  ZK_K_KINDS = 16
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];
@@ -99,6 +100,14 @@ int zk_ctx_set_timing(zk_ctx* ctx, int enable);                /* all kinds on /
 int zk_ctx_set_timing_mask(zk_ctx* ctx, uint32_t kind_mask);   /* bit k = time ZK_K_k launches */
 int zk_ctx_get_stats(const zk_ctx* ctx, zk_stats* out);
 int zk_ctx_reset_stats(zk_ctx* ctx);
+/* The event-timed launches since the last zk_ctx_reset_stats, in launch order
+ * (kind, duration, algorithmic bytes): *n gets the count, at most cap are copied. */
+typedef struct {
+  int kind;
+  double ms;
+  double alg_bytes;
+} zk_launch;
+int zk_ctx_get_launches(const zk_ctx* ctx, zk_launch* out, size_t cap, size_t* n);
 
 /* ---------------------------------------------------------------------------
  * Fiat-Shamir transcript (host) — fiat_shamir/src/fiat_shamir_transcript.rs

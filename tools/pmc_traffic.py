@@ -8,7 +8,8 @@ MI355X_MICROARCH.md "HBM") beside the algorithmic bytes of the step schedule
 (host.hpp gkr_phase): round 0 256 B per pair, a single round 768 B per output
 pair, a double step 1536 B (one pending challenge) or 2560 B (two) per quad,
 the persistent tail the sum of its double steps; k_gkr_d0m 128 B per input
-index, k_gkr_dm 2560 B per quad.
+index, k_gkr_dm 2560 B per quad, k_gkr_d0t 128 B per input index, k_gkr_t33
+9216 B per octant of its output level, k_gkr_dm3 4608 B per quad.
 Writes profiles/<tag>_traffic.json and copies the kernel-stats CSV.
 usage: python tools/pmc_traffic.py <tag> <nvars> [dtail_max_quads]
 (tools/profile_bench.sh launches steps one at a time, ZK_PRELAUNCH=0: no persistent
@@ -29,12 +30,28 @@ def dispatches(path, counter):
     return [out[k] for k in sorted(out)]
 
 
-def schedule(n, dtail_max_quads=4096, d0=True, dm_min_quads=1 << 17):
-    """(symbol prefix, algorithmic bytes) per dispatch of one proof (one GPU).
-    d0 (ZK_D0, default): an even n starts with k_gkr_d0m (rounds 0 and 1, 128 B per
-    input index) and every double step then folds by two pending challenges; those
-    with >= dm_min_quads quads run as k_gkr_dm (matrix cores), the others as k_gkr_dround."""
-    if d0 and n >= 2 and n % 2 == 0:
+def schedule(n, dtail_max_quads=4096, d0=True, dm_min_quads=1 << 17, d0t=True):
+    """(symbol prefix, algorithmic bytes) per dispatch of one proof (one GPU), as
+    host.hpp gkr_phase builds it. d0t (ZK_D0T, default, n >= 11): k_gkr_d0t
+    (rounds 0-2, 128 B per input index), nt k_gkr_t33 (9216 B per octant), one
+    k_gkr_dm3 (4608 B per quad), then double steps with two pending challenges.
+    Else d0 (ZK_D0): an even n starts with k_gkr_d0m (rounds 0 and 1). Double
+    steps with >= dm_min_quads quads run as k_gkr_dm, the others as k_gkr_dround."""
+    i, np_ = 0, 0
+    if d0t and n >= 11:
+        nt, k = -1, 0
+        while 3 + 3 * k + 8 <= n:
+            r = n - 3 - 3 * k
+            if r % 2 == 0 and (r >= 12 or nt < 0):
+                nt = k
+            k += 1
+        st = [("zk::k_gkr_d0t", 128.0 * (1 << n))]
+        for k in range(nt):
+            st.append(("zk::k_gkr_t33", 9216.0 * (1 << (n - 3 - 3 * k)) / 8))
+        i = 3 + 3 * nt
+        st.append(("zk::k_gkr_dm3", 4608.0 * (1 << (n - i)) / 4))
+        i, np_ = i + 2, 2
+    elif d0 and n >= 2 and n % 2 == 0:
         st = [("zk::k_gkr_d0m", 128.0 * (1 << n))]
         i, np_ = 2, 2
     else:
@@ -90,12 +107,22 @@ def main():
         return {"launches": len(rs), "traffic_bytes_per_launch": t / max(1, len(rs)),
                 "alg_bytes_per_launch": a / max(1, len(rs)), "traffic_over_alg": t / a if a else None}
 
-    if any(sym == "zk::k_gkr_dm" for sym, _ in sched):  # the kind with the most time (bench.py's dominant kernel)
-        big, name, kind = summary(lambda k: k.startswith("zk::k_gkr_dm")), "k_gkr_dm", "gkr_dm"
+    # the longest launch (bench.py's dominant kernel): the first k_gkr_t33 (over the inputs)
+    t33 = [r for r in steps if r["kernel"].startswith("zk::k_gkr_t33")]
+    if t33:
+        r0 = t33[0]
+        big = {"launches": 1, "traffic_bytes_per_launch": r0["fetch_bytes"] + r0["write_bytes"],
+               "alg_bytes_per_launch": r0["alg_bytes"],
+               "traffic_over_alg": (r0["fetch_bytes"] + r0["write_bytes"]) / r0["alg_bytes"]}
+        name, kind = "k_gkr_t33 (over the input tables)", "gkr_t33"
     else:
         big, name, kind = summary(lambda k: k.startswith(first)), first[4:], "gkr_d0"
     res = {"kernel": name, "kind": kind, "nvars": nvars, **big,
-           "others": {"k_gkr_d0m": summary(lambda k: "k_gkr_d0m" in k),
+           "others": {"k_gkr_d0t": summary(lambda k: "k_gkr_d0t" in k),
+                      "k_gkr_t33": summary(lambda k: "k_gkr_t33" in k),
+                      "k_gkr_dm3": summary(lambda k: "k_gkr_dm3" in k),
+                      "k_gkr_dm": summary(lambda k: k.startswith("zk::k_gkr_dm<")),
+                      "k_gkr_d0m": summary(lambda k: "k_gkr_d0m" in k),
                       "k_gkr_round0": summary(lambda k: "k_gkr_round0" in k),
                       "k_gkr_round": summary(lambda k: k.startswith("zk::k_gkr_round<")),
                       "k_gkr_dround": summary(lambda k: "k_gkr_dround" in k),

@@ -193,7 +193,9 @@ struct zk_ctx {
   struct Pending {
     int kind;
     hipEvent_t a, b;
+    double bytes;
   };
+  std::vector<zk_launch> launch_log;  // event-timed launches since the last stats reset
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_free;
   std::vector<Pending> pending;
   // communicator
@@ -276,7 +278,7 @@ uint32_t grid_for(zk_ctx* c, uint64_t work, K kernel) {
 // events on c->stream (hipExtLaunchKernelGGL: no extra API calls per launch).
 template <class Kern, class... Args>
 void launch(zk_ctx* c, int kind, double bytes, double muls, Kern kernel, uint32_t grid, Args... args) {
-  zk_ctx::Pending p{kind, nullptr, nullptr};
+  zk_ctx::Pending p{kind, nullptr, nullptr, bytes};
   const bool timed = (c->timing >> kind) & 1u;
   if (timed) {
     if (c->ev_free.empty()) {
@@ -309,6 +311,7 @@ inline void flush_timing(zk_ctx* c) {
     HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
     if (dbg) fprintf(stderr, "zk: kind %d %.1f us\n", p.kind, ms * 1e3);
     c->stats.kernel_ms[p.kind] += ms;
+    c->launch_log.push_back(zk_launch{p.kind, (double)ms, p.bytes});
     c->ev_free.push_back({p.a, p.b});
   }
   c->pending.clear();
@@ -774,7 +777,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         const uint64_t O = size / 8, nch = O / 32;
         const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F>);
         const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax);
-        launch(c, ZK_K_GKR_DM, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
+        launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
                nx[1], nx[2], nx[3], O, din, sk);
         for (int t = 0; t < 4; ++t) cur[t] = nx[t];
         enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);

@@ -123,6 +123,14 @@ int zk_ctx_reset_stats(zk_ctx* c) {
   return guarded([&] {
     require(c, "ctx is null");
     c->stats = zk_stats{};
+    c->launch_log.clear();
+  });
+}
+int zk_ctx_get_launches(const zk_ctx* c, zk_launch* out, size_t cap, size_t* n) {
+  return guarded([&] {
+    require(c && n && (out || cap == 0), "null argument");
+    *n = c->launch_log.size();
+    for (size_t i = 0; i < cap && i < c->launch_log.size(); ++i) out[i] = c->launch_log[i];
   });
 }
 

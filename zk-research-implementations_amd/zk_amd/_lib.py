@@ -17,8 +17,8 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-ABI_VERSION = 10  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
-KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm"]
+ABI_VERSION = 11  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
+KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33"]
 
 
 class ZkError(RuntimeError):
@@ -40,6 +40,10 @@ class ZkStats(C.Structure):
     ]
 
 
+class ZkLaunch(C.Structure):
+    _fields_ = [("kind", C.c_int), ("ms", C.c_double), ("alg_bytes", C.c_double)]
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t)
 
 # name -> (restype, argtypes); every symbol declared in include/zk_sumcheck.h
@@ -53,6 +57,7 @@ SIGNATURES = {
     "zk_ctx_set_timing_mask": (I, [P, U32]),
     "zk_ctx_get_stats": (I, [P, C.POINTER(ZkStats)]),
     "zk_ctx_reset_stats": (I, [P]),
+    "zk_ctx_get_launches": (I, [P, P, SZ, C.POINTER(SZ)]),
     "zk_transcript_new": (P, []),
     "zk_transcript_clone": (P, [P]),
     "zk_transcript_free": (None, [P]),

@@ -66,6 +66,14 @@ class Context:
             "host_work_us": float(s.host_work_us),
         }
 
+    def launches(self) -> list:
+        """Event-timed launches since the last reset_stats, in order: (kind, ms, alg_bytes)."""
+        n = C.c_size_t(0)
+        check(lib().zk_ctx_get_launches(self.h, None, 0, C.byref(n)))
+        arr = (_lib.ZkLaunch * max(1, n.value))()
+        check(lib().zk_ctx_get_launches(self.h, arr, n.value, C.byref(n)))
+        return [{"kind": KERNEL_KINDS[a.kind], "ms": a.ms, "alg_bytes": a.alg_bytes} for a in arr[: n.value]]
+
     # ---- device tables ----
     def alloc(self, field: int, count: int) -> "DeviceTable":
         return DeviceTable(self, field, count)
