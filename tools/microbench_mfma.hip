@@ -7,6 +7,10 @@
 //   5. k_dm_pattern: the memory side of k_gkr_dm alone (per wave: one table, per
 //      64-quad chunk and corner four loads at quarter offsets + one store; xor
 //      instead of arithmetic) at the 24-variable first double step (Q = 2^20).
+//   6. k_t33_pattern: the memory side of k_gkr_t33 alone (per wave one table; per
+//      chunk of 32 octants four folds, each 8 inputs 8 O apart -> one output;
+//      xor instead of arithmetic) at the 24-variable first triple step (O = 2^18),
+//      by grid size and by blocks per CU.
 //   3. k_dot: sum_j A_j * S_j over 256-bit values through signed 8-bit digits,
 //      an LDS row image, transposed reads and the i8 MFMA, checked exactly
 //      against a CPU big-integer sum, and timed at 2^24 elements per table.
@@ -78,6 +82,120 @@ __global__ __launch_bounds__(256) void k_dm_pattern(const uint4* const* in, uint
       }
       X2[2 * i] = a;
       X2[2 * i + 1] = b;
+    }
+  }
+}
+
+// ---- 6. memory-only k_gkr_t33 pattern
+template <int PF>
+__global__ __launch_bounds__(256) void k_t33_pattern(const uint4* const* in, uint4* const* out, size_t O) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, ql = l & 31, hh = l >> 5;
+  const uint4* X = in[w];
+  uint4* X2 = out[w];
+  const size_t nch = O / 32, h8 = 8 * O;
+  for (size_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    for (int f = 0; f < 4; ++f) {
+      const size_t e = ch * 32 + ql + (size_t)(2 * f + hh) * O;
+      uint4 a = X[2 * e], b = X[2 * e + 1];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        const uint4 c = X[2 * (e + k * h8)], d = X[2 * (e + k * h8) + 1];
+        a.x ^= c.x; a.y ^= c.y; a.z ^= c.z; a.w ^= c.w;
+        b.x ^= d.x; b.y ^= d.y; b.z ^= d.z; b.w ^= d.w;
+      }
+      X2[2 * e] = a;
+      X2[2 * e + 1] = b;
+    }
+  }
+}
+
+// variants of the store: 0 none (reads only; a data-dependent guard keeps the loads), 1 nontemporal
+template <int MODE>
+__global__ __launch_bounds__(256) void k_t33_pattern_st(const uint4* const* in, uint4* const* out, size_t O) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, ql = l & 31, hh = l >> 5;
+  const uint4* X = in[w];
+  uint4* X2 = out[w];
+  const size_t nch = O / 32, h8 = 8 * O;
+  for (size_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    for (int f = 0; f < 4; ++f) {
+      const size_t e = ch * 32 + ql + (size_t)(2 * f + hh) * O;
+      uint4 a = X[2 * e], b = X[2 * e + 1];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        const uint4 c = X[2 * (e + k * h8)], d = X[2 * (e + k * h8) + 1];
+        a.x ^= c.x; a.y ^= c.y; a.z ^= c.z; a.w ^= c.w;
+        b.x ^= d.x; b.y ^= d.y; b.z ^= d.z; b.w ^= d.w;
+      }
+      if (MODE == 0) {
+        if ((a.x ^ b.y) == 0x12345678u) X2[2 * e] = a;  // practically never
+      } else if (MODE == 2) {
+        // lane pairs trade halves so one store instruction covers contiguous 512 B per 32 lanes:
+        // even lane l stores the low halves of elements l, l+1, odd lane the high halves
+        const bool odd = l & 1;
+        uint4 pa, pb;  // partner's a (low half) and b (high half)
+        pa.x = __shfl_xor(a.x, 1); pa.y = __shfl_xor(a.y, 1); pa.z = __shfl_xor(a.z, 1); pa.w = __shfl_xor(a.w, 1);
+        pb.x = __shfl_xor(b.x, 1); pb.y = __shfl_xor(b.y, 1); pb.z = __shfl_xor(b.z, 1); pb.w = __shfl_xor(b.w, 1);
+        const size_t e0 = e & ~(size_t)1;  // the pair's first element
+        // store 1: element e0 (both halves, by the two lanes); store 2: element e0 + 1
+        X2[2 * e0 + (odd ? 1 : 0)] = odd ? pb : a;       // even: own low half of e0; odd: partner(e0) high half
+        X2[2 * (e0 + 1) + (odd ? 1 : 0)] = odd ? b : pa;  // even: partner(e0+1) low; odd: own high of e0+1
+      } else {
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        const u4v av = {a.x, a.y, a.z, a.w}, bv = {b.x, b.y, b.z, b.w};
+        __builtin_nontemporal_store(av, reinterpret_cast<u4v*>(&X2[2 * e]));
+        __builtin_nontemporal_store(bv, reinterpret_cast<u4v*>(&X2[2 * e + 1]));
+      }
+    }
+  }
+}
+
+// variants of the loads: nontemporal input loads (do not keep the 2 GiB stream in the caches) with
+// plain (SMODE 0) or nontemporal (SMODE 1) stores
+template <int SMODE>
+__global__ __launch_bounds__(256) void k_t33_pattern_ntld(const uint4* const* in, uint4* const* out, size_t O) {
+  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, ql = l & 31, hh = l >> 5;
+  const u4v* X = reinterpret_cast<const u4v*>(in[w]);
+  u4v* X2 = reinterpret_cast<u4v*>(out[w]);
+  const size_t nch = O / 32, h8 = 8 * O;
+  for (size_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    for (int f = 0; f < 4; ++f) {
+      const size_t e = ch * 32 + ql + (size_t)(2 * f + hh) * O;
+      u4v a = __builtin_nontemporal_load(&X[2 * e]), b = __builtin_nontemporal_load(&X[2 * e + 1]);
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        a ^= __builtin_nontemporal_load(&X[2 * (e + k * h8)]);
+        b ^= __builtin_nontemporal_load(&X[2 * (e + k * h8) + 1]);
+      }
+      if (SMODE == 0) {
+        X2[2 * e] = a;
+        X2[2 * e + 1] = b;
+      } else {
+        __builtin_nontemporal_store(a, &X2[2 * e]);
+        __builtin_nontemporal_store(b, &X2[2 * e + 1]);
+      }
+    }
+  }
+}
+
+// variant: lanes = 64 consecutive octants of one corner (2 KB contiguous per input), 8 folds per chunk
+__global__ __launch_bounds__(256) void k_t33_pattern64(const uint4* const* in, uint4* const* out, size_t O) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* X = in[w];
+  uint4* X2 = out[w];
+  const size_t nch = O / 64, h8 = 8 * O;
+  for (size_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    for (int f = 0; f < 8; ++f) {
+      const size_t e = ch * 64 + l + (size_t)f * O;
+      uint4 a = X[2 * e], b = X[2 * e + 1];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        const uint4 c = X[2 * (e + k * h8)], d = X[2 * (e + k * h8) + 1];
+        a.x ^= c.x; a.y ^= c.y; a.z ^= c.z; a.w ^= c.w;
+        b.x ^= d.x; b.y ^= d.y; b.z ^= d.z; b.w ^= d.w;
+      }
+      X2[2 * e] = a;
+      X2[2 * e + 1] = b;
     }
   }
 }
@@ -315,6 +433,91 @@ int main() {
       ms /= 5;
       const double bytes = 4.0 * (16 * Q + 4 * Q) * 32;
       printf("k_dm_pattern Q=2^20 grid %d: %.1f us, %.2f TB/s (%.2f GB)\n", grid, ms * 1e3, bytes / (ms * 1e-3) / 1e12, bytes / 1e9);
+    }
+  }
+  // ---- 6
+  {
+    const size_t O = (size_t)1 << 18;
+    uint4 *hin[4], *hout[4];
+    for (int t = 0; t < 4; ++t) {
+      CK(hipMalloc(&hin[t], 64 * O * 32));
+      CK(hipMalloc(&hout[t], 8 * O * 32));
+      CK(hipMemset(hin[t], t + 1, 64 * O * 32));
+    }
+    const uint4** din;
+    uint4** dout;
+    CK(hipMalloc(&din, sizeof hin));
+    CK(hipMalloc(&dout, sizeof hout));
+    CK(hipMemcpy(din, hin, sizeof hin, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dout, hout, sizeof hout, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int grid : {256, 512, 1024, 2048}) {
+      for (int it = 0; it < 2; ++it) k_t33_pattern<0><<<grid, 256>>>(din, dout, O);
+      CK(hipEventRecord(e0));
+      for (int it = 0; it < 5; ++it) k_t33_pattern<0><<<grid, 256>>>(din, dout, O);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double bytes = 4.0 * (64 * O + 8 * O) * 32;
+      printf("k_t33_pattern O=2^18 grid %d: %.1f us, %.2f TB/s (%.2f GB)\n", grid, ms * 1e3, bytes / (ms * 1e-3) / 1e12, bytes / 1e9);
+    }
+    for (int grid : {256, 512, 1024}) {
+      for (int it = 0; it < 2; ++it) k_t33_pattern64<<<grid, 256>>>(din, dout, O);
+      CK(hipEventRecord(e0));
+      for (int it = 0; it < 5; ++it) k_t33_pattern64<<<grid, 256>>>(din, dout, O);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double bytes = 4.0 * (64 * O + 8 * O) * 32;
+      printf("k_t33_pattern64 (64 octants x one corner per fold) grid %d: %.1f us, %.2f TB/s\n", grid, ms * 1e3, bytes / (ms * 1e-3) / 1e12);
+    }
+    for (int mode = 0; mode < 3; ++mode) {
+      const int grid = 512;
+      auto run = [&] {
+        if (mode == 0) k_t33_pattern_st<0><<<grid, 256>>>(din, dout, O);
+        else if (mode == 1) k_t33_pattern_st<1><<<grid, 256>>>(din, dout, O);
+        else k_t33_pattern_st<2><<<grid, 256>>>(din, dout, O);
+      };
+      for (int it = 0; it < 2; ++it) run();
+      CK(hipEventRecord(e0));
+      for (int it = 0; it < 5; ++it) run();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double rb = 4.0 * 64 * O * 32, wb = mode ? 4.0 * 8 * O * 32 : 0.0;
+      printf("k_t33_pattern %s grid %d: %.1f us, %.2f TB/s (%.2f GB)\n",
+             mode == 0 ? "reads only" : (mode == 1 ? "nontemporal stores" : "paired-lane contiguous stores"),
+             grid, ms * 1e3, (rb + wb) / (ms * 1e-3) / 1e12, (rb + wb) / 1e9);
+    }
+    for (int mode = 0; mode < 2; ++mode) {
+      const int grid = 512;
+      auto run = [&] {
+        if (mode == 0) k_t33_pattern_ntld<0><<<grid, 256>>>(din, dout, O);
+        else k_t33_pattern_ntld<1><<<grid, 256>>>(din, dout, O);
+      };
+      for (int it = 0; it < 2; ++it) run();
+      CK(hipEventRecord(e0));
+      for (int it = 0; it < 5; ++it) run();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 5;
+      const double bytes = 4.0 * (64 * O + 8 * O) * 32;
+      printf("k_t33_pattern nontemporal loads, %s stores grid %d: %.1f us, %.2f TB/s\n", mode ? "nontemporal" : "plain",
+             grid, ms * 1e3, bytes / (ms * 1e-3) / 1e12);
+    }
+    for (int t = 0; t < 4; ++t) {
+      CK(hipFree(hin[t]));
+      CK(hipFree(hout[t]));
     }
   }
   return 0;
