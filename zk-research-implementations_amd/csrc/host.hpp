@@ -774,11 +774,21 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.rab = rb;  // carries r_{i-1} for this step
       }
       if (st.kind == GS_T33) {  // rounds i .. i+2 over level i's octants: 27 moment sums
-        const uint64_t O = size / 8, nch = O / 32;
-        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F>);
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax);
-        launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
-               nx[1], nx[2], nx[3], O, din, sk);
+        const uint64_t O = size / 8;
+        // 64-octant chunks while they still give every CU a chunk, else 32 (twice the blocks)
+        if (O / 64 >= (uint64_t)c->num_cus) {
+          const uint64_t nch = O / 64;
+          const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64>);
+          const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
+          launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64>, grid, cur[0], cur[1], cur[2], cur[3],
+                 nx[0], nx[1], nx[2], nx[3], O, din, sk);
+        } else {
+          const uint64_t nch = O / 32;
+          const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 32>);
+          const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kT33ChunksMax<32> - 1) / zk::kT33ChunksMax<32>);
+          launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 32>, grid, cur[0], cur[1], cur[2], cur[3],
+                 nx[0], nx[1], nx[2], nx[3], O, din, sk);
+        }
         for (int t = 0; t < 4; ++t) cur[t] = nx[t];
         enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
         return;
