@@ -1087,7 +1087,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     for (size_t si = 0; si < ns; ++si) {
       if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
-      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0;  // no challenge to wait for
+      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T;  // no challenge to wait for
       fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f\n", si,
               steps[si].kind, steps[si].i, prev_pub ? (row[0] - prev_pub) * 0.01 : 0.0,
               first ? 0.0 : (row[1] - row[0]) * 0.01, (row[2] - (first ? row[0] : row[1])) * 0.01);
