@@ -466,7 +466,8 @@ def main() -> None:
     # the dominant kernel: the longest launch of the timed proof (k_gkr_t33 over
     # the input tables at n = 24: rounds 3-5)
     launches = ctx.launches()
-    top = max(launches, key=lambda x: x["ms"])
+    # --no-events: no launch was timed; the roofline fields then read 0
+    top = max(launches, key=lambda x: x["ms"]) if launches else {"kind": "none", "ms": 0.0, "alg_bytes": 0.0}
     dom = top["kind"]
     all_b = sum(kind(nm)["alg_bytes"] for nm in per_kind)
     all_ms = sum(kind(nm)["ms"] for nm in per_kind)

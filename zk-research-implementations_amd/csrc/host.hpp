@@ -217,6 +217,9 @@ struct zk_ctx {
   bool circuit_dense = false;  // circuit GKR: dense L^2 layer tables instead of the two-phase prover (ZK_CIRCUIT_DENSE)
   uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
   uint64_t* tail_trace = nullptr;      // ZK_DEBUG_TAIL: pinned per-round stamps of the tail kernel, printed per proof
+  uint64_t* block_trace = nullptr;     // ZK_DEBUG_BLOCKS=<step>: pinned per-block stamps of that step (needs ZK_DEBUG_TAIL)
+  int block_trace_step = -1;
+  uint32_t atomic_fanin = 1024;  // ZK_ATOMIC_FANIN: grids up to this many blocks fan in through u64 atomics
   uint32_t rtag = 0;        // last tag handed to a pre-enqueued round kernel
   void* user = nullptr;
   ncclComm_t nccl = nullptr;
@@ -235,6 +238,7 @@ namespace zkh {
 // (<= 256 ranks x 256 B), then the tail's 4 local elements and the gathered
 // 4 x world tables
 constexpr size_t kSmallBytes = 160 * 1024;
+constexpr size_t kBlockTraceMax = 8192;  // ZK_DEBUG_BLOCKS: blocks traced
 inline uint64_t* d_red(zk_ctx* c) { return reinterpret_cast<uint64_t*>(c->small.p); }
 inline uint32_t* d_flag(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 2048); }
 inline uint32_t* d_counter(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(c->small.p) + 2560); }
@@ -358,6 +362,8 @@ inline void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
 inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   zk::RoundSink s;
   s.trace = c->tail_trace ? c->tail_trace + 512 : nullptr;  // ZK_DEBUG_TAIL: per-step stamps
+  s.btrace = nullptr;
+  s.atomic_max = c->atomic_fanin;
   s.partials = reinterpret_cast<uint64_t*>(c->partials.p);
   s.counter = d_counter(c);
   s.accum = d_accum(c);
@@ -677,6 +683,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint64_t size = L >> i;  // table length in round i
     const uint64_t h = size / 2;   // pairs
     sinks[i] = make_sink(c, across_ranks);
+    if (c->block_trace && (int)si == c->block_trace_step) sinks[i].btrace = c->block_trace;
     const zk::RoundSink& sk = sinks[i];
     if (st.kind == GS_ROUND0) {
       const uint32_t grid = grid_for(c, 2 * h, zk::k_gkr_round0<F>);
@@ -1088,10 +1095,38 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
       const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T;  // no challenge to wait for
-      fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f\n", si,
-              steps[si].kind, steps[si].i, prev_pub ? (row[0] - prev_pub) * 0.01 : 0.0,
-              first ? 0.0 : (row[1] - row[0]) * 0.01, (row[2] - (first ? row[0] : row[1])) * 0.01);
+      const uint64_t rr = first ? row[0] : row[1];
+      fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f"
+              " (r->block 0 loop end %8.2f, ->publish %6.2f)\n", si, steps[si].kind, steps[si].i,
+              prev_pub ? (row[0] - prev_pub) * 0.01 : 0.0, first ? 0.0 : (row[1] - row[0]) * 0.01, (row[2] - rr) * 0.01,
+              row[3] > rr ? (row[3] - rr) * 0.01 : 0.0, row[3] > rr ? ((int64_t)row[2] - (int64_t)row[3]) * 0.01 : 0.0);
       prev_pub = row[2];
+      if (c->block_trace && (int)si == c->block_trace_step) {  // ZK_DEBUG_BLOCKS: per-block phases of this step
+        std::vector<double> le, ep, ci, fl, wd;
+        for (size_t b = 0; b < kBlockTraceMax; ++b) {
+          const uint64_t* q = c->block_trace + 8 * b;
+          if (!q[0] || !q[1] || !q[2]) continue;
+          le.push_back((double)((int64_t)q[0] - (int64_t)rr) * 0.01);
+          ep.push_back((double)((int64_t)q[1] - (int64_t)q[0]) * 0.01);
+          ci.push_back((double)((int64_t)q[2] - (int64_t)q[1]) * 0.01);
+          if (q[4] && q[5]) {
+            fl.push_back((double)((int64_t)q[4] - (int64_t)q[0]) * 0.01);
+            wd.push_back((double)((int64_t)q[5] - (int64_t)q[4]) * 0.01);
+          }
+        }
+        auto pr = [](const char* what, std::vector<double> v) {
+          if (v.empty()) return;
+          std::sort(v.begin(), v.end());
+          fprintf(stderr, "    %-22s min %8.2f  p10 %8.2f  med %8.2f  p90 %8.2f  max %8.2f us (%zu blocks)\n", what, v.front(),
+                  v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back(), v.size());
+        };
+        pr("r -> loop end", le);
+        pr("loop end -> epilogue", ep);
+        pr("epilogue -> counted in", ci);
+        pr("loop end -> flushed", fl);
+        pr("flushed -> words", wd);
+        memset(c->block_trace, 0, kBlockTraceMax * 64);
+      }
     }
   }
   if (c->tail_trace && !steps.empty() && steps.back().kind == GS_TAIL) {  // ZK_DEBUG_TAIL

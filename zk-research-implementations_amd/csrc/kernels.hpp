@@ -167,7 +167,9 @@ __device__ __forceinline__ Fe fold2c(const Fe& x00, const Fe& x01, const Fe& x10
 // carry propagation + REDC. The multi-GPU all-reduce sums the same u64 vector.
 //
 // Cross-block fan-in: a single block publishes directly; up to
-// kAtomicFaninMax blocks add their limb sums with u64 atomics and count in;
+// RoundSink::atomic_max blocks (1024 by default, ZK_ATOMIC_FANIN) add their
+// limb sums with u64 atomics and count in (measured 11 us per 24-var proof
+// faster than the two-level fan-in for the 256-512-block matrix-core grids);
 // larger grids meet in two levels (blockIdx % 8 shards, then a top counter)
 // through per-block slots written/read with write-through (sc1) 8-byte
 // accesses (MI355X_MICROARCH.md "Valid forms": no release/acquire fence, so
@@ -206,7 +208,11 @@ struct RoundSink {
   uint32_t* host_flag;  // pinned host word, or null
   uint32_t tag;
   uint64_t* trace;      // debug (ZK_DEBUG_TAIL): 4 s_memrealtime stamps per tag (entry, challenge, publish), or null
+  uint64_t* btrace;     // debug (ZK_DEBUG_BLOCKS): 8 words per block (stamps: main loop end, fan-in start, counted in; chunk count; flushed, words), or null
+  uint32_t atomic_max;  // grids up to this many blocks fan in through u64 atomics (ZK_ATOMIC_FANIN)
 };
+#define ZK_BLOCK_STAMP(sk, i) \
+  do { if ((sk).btrace && threadIdx.x == 0 && blockIdx.x < 8192) (sk).btrace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 // block 0 / the publishing block stamps slot i of this sink's trace row
 #define ZK_SINK_STAMP(sk, i) \
   do { if ((sk).trace && threadIdx.x == 0) (sk).trace[((sk).tag & 63) * 4 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -389,7 +395,6 @@ __device__ __forceinline__ void sum_slots(uint64_t* slots, uint32_t first, uint3
   }
 }
 
-constexpr uint32_t kAtomicFaninMax = 64;  // grids up to this size fan in through u64 atomics
 
 // Block limb sums are in sc.tot[0..C) (valid for threads < C); finish over the grid.
 // G: the blocks taking part (blocks 0 .. G-1; default the whole grid).
@@ -398,6 +403,7 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk, uint32_
   static_assert(C <= kSlotU64 && C <= kBlock, "limb vector too long");
   if (G == 0) G = gridDim.x;
   const uint32_t t = threadIdx.x;
+  ZK_BLOCK_STAMP(sk, 1);
   if (G == 1) {
     ZK_STAMP(4);
     ZK_STAMP(5);
@@ -405,7 +411,7 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk, uint32_
     ZK_STAMP(6);
     return;
   }
-  if (G <= kAtomicFaninMax) {
+  if (G <= sk.atomic_max) {
     // every block adds its limb sums (no-return u64 atomics, device-coherent
     // level; G * 256 * 2^32 < 2^64 stays exact), drains, and counts in
     if (t < (uint32_t)C) __hip_atomic_fetch_add(sk.accum + t, sc.tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,6 +423,7 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk, uint32_
     }
     __syncthreads();
     ZK_STAMP(4);
+    ZK_BLOCK_STAMP(sk, 2);
     if (!sc.am_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (t < (uint32_t)C)  // read and re-arm for the next launch
@@ -439,6 +446,7 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk, uint32_
   }
   __syncthreads();
   ZK_STAMP(4);
+  ZK_BLOCK_STAMP(sk, 2);
   if (!sc.am_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the add
   sum_slots<C>(sk.partials, shard, 8u, in_shard, sc);

@@ -466,7 +466,8 @@ __device__ __forceinline__ void dm_products(const Fe (&z)[4], DMScratch& sc, i32
 // tiles -> anti-diagonal sums -> 17 words per category -> grid limb sums
 template <class F>
 __device__ __forceinline__ void dm_epilogue(const i32x16 (&acc)[4], DMScratch& sc, const RoundSink& sink) {
-  const uint32_t t = threadIdx.x, l = t & 63, cg = t >> 7, col = l & 31, h = l >> 5;
+  const uint32_t t = threadIdx.x;
+  const uint32_t l = t & 63, cg = t >> 7, col = l & 31, h = l >> 5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -491,7 +492,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, 
   block_get_rs(din, ra, rb, rab, gridDim.x > 1);
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ DMScratch sc;
-  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, pp = w & 1, cg = w >> 1;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
   if (t < 96) {
     const uint32_t c = t >> 5, k = t & 31;
     dm_row<F>(sc.wimg[c][k], fe_mul<F>(c == 0 ? ra : (c == 1 ? rb : rab), p2dig<F>(k)));
@@ -528,6 +529,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, 
     }
     dm_products<F>(z, sc, acc);
   }
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
+  ZK_BLOCK_STAMP(sink, 0);
   dm_epilogue<F>(acc, sc, sink);
 }
 
@@ -672,6 +675,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
     __syncthreads();  // the image of this chunk is complete (double buffering: one barrier per chunk)
     d0t_mfmas(sc.img[buf], acc);
   }
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
+  ZK_BLOCK_STAMP(sink, 0);
   __syncthreads();
   d0t_flush(acc, sc.T);
   __syncthreads();
@@ -779,6 +784,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm3(const Fe* __restrict__ A,
     }
     dm_products<F>(z, sc, acc);
   }
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
+  ZK_BLOCK_STAMP(sink, 0);
   dm_epilogue<F>(acc, sc, sink);
 }
 
@@ -820,10 +827,28 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
                                                       Fe* __restrict__ P2, uint64_t O, DIn din, RoundSink sink) {
   Fe ra, rb, rc;
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
+  const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
+  Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
+  const uint64_t nch = O / OCT, h8 = 8 * O;  // level-i tables hold 8 O elements
+  // fold f's inputs: OCT 64: corner f of octants ch*64 + l; OCT 32: corner 2f + hh of octants ch*32 + ql
+  auto in_at = [&](uint64_t ch, int f, Fe (&x)[8]) {
+    const uint64_t e = OCT == 64 ? ch * 64 + l + (uint64_t)f * O : ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
+  };
+  // inputs two folds ahead (one wave per SIMD: the loads in flight are what
+  // hides HBM latency). OCT 64: the first two folds' inputs (written by the
+  // previous kernel) are in flight while the host posts the challenges (OCT
+  // 32 loads them after the constants: held across them it spills)
+  Fe nx[8], nx2[8];
+  if (OCT == 64 && (uint64_t)blockIdx.x < nch) {
+    in_at(blockIdx.x, 0, nx);
+    in_at(blockIdx.x, 1, nx2);
+  }
   block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc for this step
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ T33Scratch sc;
-  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
   if (t < 8) {  // eq((ra, rb, rc), c), c = 4a + 2b + c0
     const Fe one = fe_one<F>();
     const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
@@ -839,8 +864,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
 #pragma unroll
   for (int c = 0; c < 8; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
   __syncthreads();
-  const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
-  Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
   i32x16 acc[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
@@ -848,18 +871,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     for (int r = 0; r < 16; ++r) acc[i][r] = 0;
   if constexpr (OCT == 64) {
   uint8_t(*img)[4][64][32] = reinterpret_cast<uint8_t(*)[4][64][32]>(&sc.img[0][0][0][0][0]);
-  const uint64_t nch = O / 64, h8 = 8 * O;  // level-i tables hold 8 O elements
-  auto in_at = [&](uint64_t ch, int f, Fe (&x)[8]) {  // fold f = corner f of octants ch*64 + l
-    const uint64_t e = ch * 64 + l + (uint64_t)f * O;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
-  };
-  // inputs two folds ahead (one wave per SIMD: the loads in flight are what hides HBM latency)
-  Fe nx[8], nx2[8];
-  if ((uint64_t)blockIdx.x < nch) {
-    in_at(blockIdx.x, 0, nx);
-    in_at(blockIdx.x, 1, nx2);
-  }
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
@@ -900,14 +911,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     __syncthreads();  // the image is rewritten by the next chunk
   }
   } else {
-  const uint64_t nch = O / 32, h8 = 8 * O;  // level-i tables hold 8 O elements
-  auto in_at = [&](uint64_t ch, int f, Fe (&x)[8]) {
-    const uint64_t e = ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
-  };
-  // inputs two folds ahead (one wave per SIMD: the loads in flight are what hides HBM latency)
-  Fe nx[8], nx2[8];
   if ((uint64_t)blockIdx.x < nch) {
     in_at(blockIdx.x, 0, nx);
     in_at(blockIdx.x, 1, nx2);
@@ -951,11 +954,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     }
   }
   }
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
+  ZK_BLOCK_STAMP(sink, 0);
   __syncthreads();
   d0t_flush(acc, sc.T);
   __syncthreads();
+  ZK_BLOCK_STAMP(sink, 4);
   if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
   __syncthreads();
+  ZK_BLOCK_STAMP(sink, 5);
   if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
   __syncthreads();
   grid_finish<kD0TLimbs>(sc, sink);

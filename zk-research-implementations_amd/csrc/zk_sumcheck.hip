@@ -54,6 +54,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_D0")) c->d0 = atoi(e);
     if (const char* e = getenv("ZK_CIRCUIT_DENSE")) c->circuit_dense = atoi(e) != 0;
     if (const char* e = getenv("ZK_DTAIL_MAX_QUADS")) c->dtail_max_quads = strtoull(e, nullptr, 0);
+    if (const char* e = getenv("ZK_ATOMIC_FANIN")) c->atomic_fanin = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_DTAIL_BLOCKS")) c->dtail_blocks = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_TAIL_MAX_PAIRS")) c->tail_max_pairs = strtoull(e, nullptr, 0);
     c->num_cus = prop.multiProcessorCount;
@@ -67,6 +68,12 @@ int zk_ctx_create(int device, zk_ctx** out) {
       if (getenv("ZK_DEBUG_TAIL")) {
         HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->tail_trace), 1024 * 8, hipHostMallocMapped | hipHostMallocCoherent));
         memset(c->tail_trace, 0, 1024 * 8);  // [0, 512): tail kernels, [512, 768): per-step stamps
+        if (const char* b = getenv("ZK_DEBUG_BLOCKS")) {
+          c->block_trace_step = atoi(b);
+          HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->block_trace), zkh::kBlockTraceMax * 64,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+          memset(c->block_trace, 0, zkh::kBlockTraceMax * 64);
+        }
       }
     } catch (...) {
       zk_ctx_destroy(c);
@@ -92,6 +99,7 @@ void zk_ctx_destroy(zk_ctx* c) {
   c->partials.release();
   c->tailbuf.release();
   if (c->tail_trace) (void)hipHostFree(c->tail_trace);
+  if (c->block_trace) (void)hipHostFree(c->block_trace);
   c->small.release();
   for (auto& b : c->msm) b.release();
   for (auto& b : c->scan_tmp) b.release();
