@@ -463,6 +463,9 @@ __device__ __forceinline__ void dm_products(const Fe (&z)[4], DMScratch& sc, i32
   }
   __syncthreads();
 }
+template <class F, int NT>
+__device__ __forceinline__ void tiles_to_words(const unsigned long long (&T)[NT][64], uint64_t (&W)[NT][17]);
+
 // tiles -> anti-diagonal sums -> 17 words per category -> grid limb sums
 template <class F>
 __device__ __forceinline__ void dm_epilogue(const i32x16 (&acc)[4], DMScratch& sc, const RoundSink& sink) {
@@ -477,7 +480,7 @@ __device__ __forceinline__ void dm_epilogue(const i32x16 (&acc)[4], DMScratch& s
     }
   }
   __syncthreads();
-  if (t < (uint32_t)kDCats) diag_to_words<F>(sc.T[t], sc.tot + t * 17);
+  tiles_to_words<F, kDCats>(sc.T, *reinterpret_cast<uint64_t(*)[kDCats][17]>(sc.tot));
   __syncthreads();
   grid_finish<kDLimbs>(sc, sink);
 }
@@ -580,6 +583,12 @@ __device__ __forceinline__ Fe p2w(uint32_t k) {  // 2^(32 (8 + k)) mod p
   else return kP2WBls12_381Fr[k];
 }
 template <class F>
+__device__ __forceinline__ uint32_t p2w_word(uint32_t k, uint32_t j) {  // word j of 2^(32 (8 + k)) mod p (dynamic j)
+  if constexpr (F::id == BN254_FR) return kP2WBn254Fr[k].v[j];
+  else if constexpr (F::id == BN254_FQ) return kP2WBn254Fq[k].v[j];
+  else return kP2WBls12_381Fr[k].v[j];
+}
+template <class F>
 __device__ __forceinline__ void words17_to_limbs9(const uint64_t* x, uint64_t* out) {
   uint64_t col[9];
 #pragma unroll
@@ -600,6 +609,51 @@ __device__ __forceinline__ void words17_to_limbs9(const uint64_t* x, uint64_t* o
   for (int j = 0; j < 9; ++j) out[j] = col[j];
 }
 
+// Block-parallel epilogue of NT tiles (the per-tile serial chains of
+// diag_to_words / words17_to_limbs9 took ~1.5 us each on one wave):
+// (tile, word) items build S_w, NT threads run the 17-step carries in place,
+// (tile, limb) items fold the high words (2 products per high word each).
+template <class F, int NT>
+__device__ __forceinline__ void tiles_to_words(const unsigned long long (&T)[NT][64], uint64_t (&W)[NT][17]) {
+  for (uint32_t it = threadIdx.x; it < (uint32_t)NT * 17; it += kBlock) {
+    const uint32_t tile = it / 17, w = it % 17;
+    int64_t v = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+      if (4 * w + i < 63) v += (int64_t)T[tile][4 * w + i] * ((int64_t)1 << (8 * i));
+    W[tile][w] = (uint64_t)v;
+  }
+  __syncthreads();
+  if (threadIdx.x < (uint32_t)NT) {
+    int64_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < 17; ++w) {
+      const int64_t v = (int64_t)W[threadIdx.x][w] + (int64_t)d0m_offset_word<F>(w) + carry;
+      W[threadIdx.x][w] = (uint32_t)v;
+      carry = v >> 32;
+    }
+  }
+  __syncthreads();
+}
+template <class F>
+__device__ __forceinline__ void stage_p2w(uint32_t (&K)[9][8]) {  // threads < 72; read after a barrier
+  if (threadIdx.x < 72) K[threadIdx.x >> 3][threadIdx.x & 7] = p2w_word<F>(threadIdx.x >> 3, threadIdx.x & 7);
+}
+template <class F, int NT>
+__device__ __forceinline__ void words_to_limbs9(const uint64_t (&W)[NT][17], const uint32_t (&K)[9][8], uint64_t* tot) {
+  for (uint32_t it = threadIdx.x; it < (uint32_t)NT * 9; it += kBlock) {
+    const uint32_t tile = it / 9, j = it % 9;
+    uint64_t col = j < 8 ? W[tile][j] : 0;
+#pragma unroll
+    for (int w = 8; w < 17; ++w) {
+      const uint32_t xw = (uint32_t)W[tile][w];
+      if (j < 8) col += (uint32_t)((uint64_t)xw * K[w - 8][j]);
+      if (j > 0) col += ((uint64_t)xw * K[w - 8][j - 1]) >> 32;
+    }
+    tot[it] = col;
+  }
+}
+
 struct D0TScratch {
   uint8_t img[2][8][2][32][32];  // buffer, corner, table (X, Y), octant, digit row (32 KiB)
   unsigned long long T[kD0TCats][64];
@@ -607,6 +661,7 @@ struct D0TScratch {
   uint64_t tot[kSlotU64];
   uint64_t pp[kBlock];
   uint32_t am_last;
+  uint32_t p2w[9][8];  // 2^(32 (8 + k)) mod p, staged at kernel start for words_to_limbs9
 };
 
 // wave w = 2 aX + aY: products X_u Y_v, u = 4 aX + ux, v = 4 aY + vy; tile slot 3 d_b + d_c
@@ -647,6 +702,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   __shared__ D0TScratch sc;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, half = l >> 5, ql = l & 31;
   for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  stage_p2w<F>(sc.p2w);
   i32x16 acc[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i)
@@ -680,9 +736,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   __syncthreads();
   d0t_flush(acc, sc.T);
   __syncthreads();
-  if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
-  __syncthreads();
-  if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
+  tiles_to_words<F, kD0TCats>(sc.T, sc.w17);
+  words_to_limbs9<F, kD0TCats>(sc.w17, sc.p2w, sc.tot);
   __syncthreads();
   grid_finish<kD0TLimbs>(sc, sink);
 }
@@ -817,6 +872,7 @@ struct T33Scratch {
   uint64_t tot[kSlotU64];
   uint64_t pp[kBlock];
   uint32_t am_last;
+  uint32_t p2w[9][8];  // 2^(32 (8 + k)) mod p, staged at kernel start for words_to_limbs9
   Fe eqw[8];
 };
 
@@ -856,6 +912,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
   }
   for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  stage_p2w<F>(sc.p2w);
   __syncthreads();
   uint8_t(*wimg)[32][32] = reinterpret_cast<uint8_t(*)[32][32]>(&sc.img[0][0][0][0][0]);
   dm_row<F>(wimg[t >> 5][t & 31], fe_mul<F>(sc.eqw[t >> 5], p2dig<F>(t & 31)));
@@ -960,10 +1017,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   d0t_flush(acc, sc.T);
   __syncthreads();
   ZK_BLOCK_STAMP(sink, 4);
-  if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
-  __syncthreads();
+  tiles_to_words<F, kD0TCats>(sc.T, sc.w17);
   ZK_BLOCK_STAMP(sink, 5);
-  if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
+  words_to_limbs9<F, kD0TCats>(sc.w17, sc.p2w, sc.tot);
   __syncthreads();
   grid_finish<kD0TLimbs>(sc, sink);
 }
@@ -1013,6 +1069,7 @@ struct TTScratch {
   uint64_t tot[kSlotU64];
   uint64_t pp[kBlock];
   uint32_t am_last;
+  uint32_t p2w[9][8];  // 2^(32 (8 + k)) mod p, staged at kernel start for words_to_limbs9
   Fe eqw[8];
 };
 
