@@ -1120,6 +1120,18 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
           fprintf(stderr, "    %-22s min %8.2f  p10 %8.2f  med %8.2f  p90 %8.2f  max %8.2f us (%zu blocks)\n", what, v.front(),
                   v[v.size() / 10], v[v.size() / 2], v[v.size() * 9 / 10], v.back(), v.size());
         };
+        if (const char* fn = getenv("ZK_DEBUG_BLOCKS_FILE")) {  // raw per-block stamps (us after r)
+          if (FILE* f = fopen(fn, "w")) {
+            fprintf(f, "block,loop_end,fanin_start,counted_in\n");
+            for (size_t b = 0; b < kBlockTraceMax; ++b) {
+              const uint64_t* q = c->block_trace + 8 * b;
+              if (!q[0] || !q[1] || !q[2]) continue;
+              fprintf(f, "%zu,%.2f,%.2f,%.2f\n", b, ((int64_t)q[0] - (int64_t)rr) * 0.01, ((int64_t)q[1] - (int64_t)rr) * 0.01,
+                      ((int64_t)q[2] - (int64_t)rr) * 0.01);
+            }
+            fclose(f);
+          }
+        }
         pr("r -> loop end", le);
         pr("loop end -> epilogue", ep);
         pr("epilogue -> counted in", ci);
