@@ -897,12 +897,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   // hides HBM latency). OCT 64: the first two folds' inputs (written by the
   // previous kernel) are in flight while the host posts the challenges (OCT
   // 32 loads them after the constants: held across them it spills)
+  // Block 0's wave 0 polls the host for the challenges and relays them to
+  // every block: its poll would wait behind these loads (vmcnt is in order),
+  // so it loads after the challenges arrive.
   Fe nx[8], nx2[8];
-  if (OCT == 64 && (uint64_t)blockIdx.x < nch) {
+  const bool early = OCT == 64 && (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
+  if (early) {
     in_at(blockIdx.x, 0, nx);
     in_at(blockIdx.x, 1, nx2);
   }
   block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc for this step
+  if (OCT == 64 && !early && (uint64_t)blockIdx.x < nch) {
+    in_at(blockIdx.x, 0, nx);
+    in_at(blockIdx.x, 1, nx2);
+  }
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ T33Scratch sc;
   if (t < 8) {  // eq((ra, rb, rc), c), c = 4a + 2b + c0
