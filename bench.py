@@ -506,7 +506,7 @@ def main() -> None:
                 "nvars_total": n,
                 "nvars_per_gpu": nloc,
                 "parallelism": f"hypercube split over {world} GPU(s) by low index bits; "
-                + ("1 RCCL all-reduce (24 x u64) per round" if args.comm == "rccl" else
+                + ("1 RCCL all-reduce of the step's limb sums (<= 243 x u64) per step of 2-3 rounds" if args.comm == "rccl" else
                    "host (gloo) all-reduce per round: diagnostic, not the product path") if world > 1 else "single GPU",
             },
             "roofline": {

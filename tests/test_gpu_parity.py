@@ -2,6 +2,8 @@
 golden vectors and the reference's own tests. Bit-exact for every output."""
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 import hashlib
 
@@ -302,12 +304,15 @@ def test_stats_and_timing(ctx):
     # rounds 0 and 1 in one pass over the inputs (k_gkr_d0r, ZK_D0 default), then
     # rounds (2,3) .. (10,11) two per step, each folding by two pending challenges
     # (the first straight from the inputs); these small steps run in one persistent
-    # kernel (k_gkr_dtail)
+    # kernel (k_gkr_dtail), except the last ZK_HOST_ROUNDS (default 4) rounds:
+    # the tail's last device step hands its tables to the host, which runs them
     assert k["gkr_d0"]["launches"] == 1 and k["gkr_dtail"]["launches"] == 1 and k["gkr_dround"]["launches"] == 0
     assert k["gkr_round0"]["launches"] + k["gkr_round"]["launches"] + k["gkr_round_lanes"]["launches"] == 0
-    q = [1 << (n - 4 - 2 * d) for d in range((n - 2) // 2)]  # quads of each double step (Z = 4Q)
+    host_rounds = int(os.environ.get("ZK_HOST_ROUNDS", "4")) & ~1
+    nd = (n - 2) // 2 - host_rounds // 2  # double steps on the device
+    q = [1 << (n - 4 - 2 * d) for d in range(nd)]  # quads of each double step (Z = 4Q)
     assert k["gkr_dtail"]["alg_bytes"] == 2560 * sum(q)
-    assert k["gkr_dtail"]["ms"] > 0 and st["host_syncs"] >= 1 + (n - 2) // 2
+    assert k["gkr_dtail"]["ms"] > 0 and st["host_syncs"] >= 1 + nd
     assert k["gkr_d0"]["alg_bytes"] == 128 * (1 << n)
 
 

@@ -15,6 +15,8 @@
 * With ZK_DROUND=0 the small rounds run in one persistent kernel (k_gkr_tail);
   the proof is identical with one launch per round (ZK_TAIL=0) and when the
   tail starts at round 1 over large tables (ZK_LANES_MAX_PAIRS).
+* The last ZK_HOST_ROUNDS rounds (default 4) run on the host from the tables
+  the persistent tail hands over; every setting gives the oracle's proof.
 * When the host fails mid-proof (here: the host all-reduce callback raises in
   round 3), the call returns ZK_ECOMM promptly — the guard releases every
   kernel still waiting instead of letting each run into its 1 s limit — and
@@ -271,3 +273,24 @@ def test_three_round_first_pass_agrees_large(monkeypatch, field, n):
         finally:
             ctx.close()
     assert got["1"] == got["0"]
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("n", [8, 10, 12, 15, 16, 19])
+def test_host_rounds_match_oracle(monkeypatch, field, n):
+    """The last ZK_HOST_ROUNDS rounds on the host (host.hpp "host rounds"): the
+    persistent tail's last device step stores its output tables word-major to
+    pinned host memory (kernels.hpp st_fe_sys) and the host folds them by that
+    step's challenges and runs the remaining rounds. Every H (0 = all on the
+    device; odd H rounds down; H larger than the schedule allows falls back to
+    the device) gives the oracle's proof, twice on one context (the host
+    table buffer is reused)."""
+    want = _oracle(field, n)
+    for h in ("0", "2", "4", "5", "6", "8", "40"):
+        monkeypatch.setenv("ZK_HOST_ROUNDS", h)
+        ctx = zk_amd.Context(0)
+        try:
+            assert _prove(ctx, field, n) == want, f"ZK_HOST_ROUNDS={h}"
+            assert _prove(ctx, field, n) == want, f"ZK_HOST_ROUNDS={h} (second proof)"
+        finally:
+            ctx.close()

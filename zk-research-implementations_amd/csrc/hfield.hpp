@@ -98,6 +98,52 @@ inline V reduce(V x) {  // any 256-bit x -> x mod p (2^256 < 6p)
   for (int k = 0; k < 5; ++k) x = sub_p_if_ge<F>(x);
   return x;
 }
+// Montgomery reduction of a 512-bit T = (lo, hi) with hi < p: T R^-1 mod p
+// (T < p R, so the result before the final subtraction is < 2p)
+template <class F>
+inline V redc512(const uint64_t (&x)[8]) {
+  uint64_t t[9];
+  for (int i = 0; i < 8; ++i) t[i] = x[i];
+  t[8] = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint64_t m = t[i] * pinv<F>();
+    uint64_t c = 0;
+    for (int j = 0; j < 4; ++j) {
+      const u128 s = (u128)m * P<F>(j) + t[i + j] + c;
+      t[i + j] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    for (int k = i + 4; k < 9 && c; ++k) {
+      const u128 s = (u128)t[k] + c;
+      t[k] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+  }
+  V r = {{t[4], t[5], t[6], t[7]}};
+  return sub_p_if_ge<F>(r, t[8]);
+}
+template <class F>
+inline bool lt_p(const uint64_t* x) {  // x[0..3] < p
+  unsigned long b = 0;
+  for (int i = 0; i < 4; ++i) (void)__builtin_subcl(x[i], P<F>(i), b, &b);
+  return b != 0;
+}
+// acc (9 limbs) += a b (512-bit product, no reduction)
+inline void mac_wide(uint64_t (&acc)[9], const V& a, const V& b) {
+  uint64_t pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) {
+    uint64_t c = 0;
+    for (int j = 0; j < 4; ++j) {
+      const u128 s = (u128)a.l[j] * b.l[i] + pr[i + j] + c;
+      pr[i + j] = (uint64_t)s;
+      c = (uint64_t)(s >> 64);
+    }
+    pr[i + 4] = c;
+  }
+  unsigned long c = 0;
+  for (int k = 0; k < 8; ++k) acc[k] = __builtin_addcl(acc[k], pr[k], c, &c);
+  acc[8] += c;
+}
 template <class F>
 inline V r2() {
   V r;
@@ -151,10 +197,24 @@ inline Fe hlimbs_to_fe(const uint64_t* w, int L, bool product) {
     ch[1].l[k] = t[4 + k];
     ch[2].l[k] = t[8 + k];
   }
+  if (product && (t[8] | t[9] | t[10] | t[11]) == 0 && h64::lt_p<F>(t + 4)) {  // T < p R: one 512-bit REDC
+    const uint64_t (&lo8)[8] = *reinterpret_cast<const uint64_t(*)[8]>(t);
+    return h64::fe(h64::redc512<F>(lo8));
+  }
   h64::V one = {{1, 0, 0, 0}};
   if (product)  // REDC(C0) + (C1 mod p) + C2 R   (mul(x, 1) is exact for any x < 2^256)
     return h64::fe(h64::add<F>(h64::add<F>(h64::mul<F>(ch[0], one), h64::reduce<F>(ch[1])),
                                h64::mul<F>(h64::reduce<F>(ch[2]), h64::r2<F>())));
   return h64::fe(h64::add<F>(h64::reduce<F>(ch[0]), h64::mul<F>(h64::reduce<F>(ch[1]), h64::r2<F>())));
+}
+// sum of products of Montgomery images accumulated by mac_wide -> Montgomery image of the field sum
+template <class F>
+inline Fe wide_to_fe(const uint64_t (&acc)[9]) {
+  uint64_t w[18];
+  for (int k = 0; k < 9; ++k) {
+    w[2 * k] = (uint32_t)acc[k];
+    w[2 * k + 1] = acc[k] >> 32;
+  }
+  return hlimbs_to_fe<F>(w, 18, true);
 }
 }  // namespace zk

@@ -213,6 +213,9 @@ struct zk_ctx {
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
+  uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
+  uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
+  size_t h_tab_bytes = 0;
   bool tail = true;         // (ZK_DROUND=0 only) pre-enqueued small rounds in one persistent kernel (ZK_TAIL=0: one launch each)
   bool circuit_dense = false;  // circuit GKR: dense L^2 layer tables instead of the two-phase prover (ZK_CIRCUIT_DENSE)
   uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
@@ -542,12 +545,50 @@ struct GStep {
 enum {
   GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5, GS_D0T = 6, GS_T32 = 7, GS_T33 = 8,
   GS_TT = 9,     // one small triple step (k_gkr_ttail, one step per launch)
-  GS_TTAIL = 10  // the small triple steps in one persistent kernel (k_gkr_ttail)
+  GS_TTAIL = 10, // the small triple steps in one persistent kernel (k_gkr_ttail)
+  GS_HOST = 11   // the last rounds on the host, from the tables the persistent tail's last step hands over
 };
+
+// Host rounds (ZK_HOST_ROUNDS, default 4; only where the caller does not
+// need the final tables, host_ok): a double step on a few-element table is
+// one wave's dependent chain of 256-bit multiplies (~7 us) plus a hand-off
+// (~5 us), while the host does the same round in about a microsecond. So
+// the persistent tail's last device step stores its output tables (4 x
+// 2^(H+2) elements, 8 KiB at H = 4) to pinned host memory, and the host folds
+// them by that step's two challenges and runs the last H rounds itself — the
+// reference's own arithmetic (gkr_prove's loop, sum_check_protocol.rs:86-115,
+// with get_round_partial_polynomial_proof_gkr :152-166 and partial_evaluate
+// multilinear_polynomial_evaluation.rs:52-63), same field values.
+template <class F>
+void host_fold(std::vector<Fe> (&T)[4], const Fe& r) {
+  for (auto& t : T) {
+    const size_t h = t.size() / 2;
+    for (size_t j = 0; j < h; ++j) t[j] = zk::hfe_add<F>(t[j], zk::hfe_mul<F>(r, zk::hfe_sub<F>(t[j + h], t[j])));
+    t.resize(h);
+  }
+}
+// e0 = sum [A S + M P](lo), e2 = sum [A S + M P](2 hi - lo) over the pairs of the current tables
+// (products summed unreduced, one reduction per value)
+template <class F>
+void host_round_sums(const std::vector<Fe> (&T)[4], Fe& e0, Fe& e2) {
+  using namespace zk;
+  const size_t h = T[0].size() / 2;
+  uint64_t a0[9] = {0}, a2[9] = {0};
+  for (size_t j = 0; j < h; ++j) {
+    h64::V x2[4];
+    for (int t = 0; t < 4; ++t) x2[t] = h64::of(hfe_sub<F>(hfe_add<F>(T[t][j + h], T[t][j + h]), T[t][j]));
+    h64::mac_wide(a0, h64::of(T[0][j]), h64::of(T[1][j]));
+    h64::mac_wide(a0, h64::of(T[2][j]), h64::of(T[3][j]));
+    h64::mac_wide(a2, x2[0], x2[1]);
+    h64::mac_wide(a2, x2[2], x2[3]);
+  }
+  e0 = wide_to_fe<F>(a0);
+  e2 = wide_to_fe<F>(a2);
+}
 
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
-               GkrOut& out, Fe& claim, Fe& r, uint32_t& pend) {
+               GkrOut& out, Fe& claim, Fe& r, uint32_t& pend, bool host_ok = false) {
   const uint64_t L = (uint64_t)1 << nv;
   const bool pre = prelaunch(c, nv);
   std::vector<GStep> steps;
@@ -613,6 +654,25 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (nv >= 3 && (nv - 2) % 2 == 1) steps.push_back({GS_SINGLE, i++, 0});
     }
     for (; i + 1 < nv; i += 2, np = 2) steps.push_back({GS_DOUBLE, i, np});
+    // host rounds: the last H rounds, if they are whole double steps and the
+    // persistent tail keeps >= 2 device steps before them
+    uint32_t hostH = 0;
+    if (host_ok && pre && c->dtail && use_tail(c, across_ranks) && !(across_ranks && multi_rank(c)) && c->host_rounds >= 2) {
+      const uint32_t H = c->host_rounds & ~1u;
+      size_t k = steps.size();
+      uint32_t got = 0;
+      while (got < H && k > 0 && steps[k - 1].kind == GS_DOUBLE && steps[k - 1].np == 2) {
+        --k;
+        got += 2;
+      }
+      size_t smalls = 0;  // device double steps left for the persistent tail
+      for (size_t q = 0; q < k; ++q)
+        if (steps[q].kind == GS_DOUBLE && (L >> steps[q].i) / 4 <= c->dtail_max_quads) ++smalls;
+      if (got == H && smalls >= 2 && k == steps.size() - H / 2) {
+        steps.resize(k);
+        hostH = H;
+      }
+    }
     // the small doubles (>= 2 of them) in one persistent kernel
     if (pre && c->dtail && use_tail(c, across_ranks)) {
       size_t d0 = 0;
@@ -627,6 +687,18 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         c->tailbuf.ensure(kTailRelayBytes + zk::dtail_region(Q0, (uint32_t)nd) * sizeof(Fe));
         if (c->tailbuf.bytes != had) HIPCK(hipMemset(c->tailbuf.p, 0, kTailRelayBytes));  // relay tags at rest
       }
+    }
+    if (hostH > 0) {
+      if (steps.empty() || steps.back().kind != GS_DTAIL) fail(ZK_EINVAL, "internal: host rounds need the persistent tail");
+      const size_t need = (size_t)4 * ((size_t)1 << (hostH + 2)) * sizeof(Fe);
+      if (c->h_tab_bytes < need) {
+        if (c->h_tab) HIPCK(hipHostFree(c->h_tab));
+        c->h_tab = nullptr;
+        c->h_tab_bytes = 0;
+        HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_tab), need, hipHostMallocMapped | hipHostMallocCoherent));
+        c->h_tab_bytes = need;
+      }
+      steps.push_back({GS_HOST, nv - hostH, 2});
     }
   } else {
     // first round >= 1 with <= tail_max_pairs pairs, if at least two rounds remain
@@ -659,7 +731,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         case GS_D0T: case GS_T33: case GS_TT: nr = 3; break;
         case GS_DTAIL: nr = 2 * st.nd; break;
         case GS_TTAIL: nr = 3 * st.nd; break;
-        case GS_TAIL: nr = nv - st.i; break;
+        case GS_TAIL: case GS_HOST: nr = nv - st.i; break;
         default: nr = 1;
       }
       if (st.i != next) fail(ZK_EINVAL, "internal: step schedule out of order");
@@ -679,6 +751,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   };
   auto enqueue = [&](size_t si) {
     const GStep& st = steps[si];
+    if (st.kind == GS_HOST) return;  // no kernel: the host runs these rounds
     const uint32_t i = st.i;
     const uint64_t size = L >> i;  // table length in round i
     const uint64_t h = size / 2;   // pairs
@@ -851,6 +924,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       c->rtag += st.nd;
       a.rtag0 = rtags[si];
       if (c->tail_trace) a.trace = c->tail_trace;
+      if (si + 1 < ns && steps[si + 1].kind == GS_HOST) a.host_tab = c->h_tab;
       const uint32_t grid = (uint32_t)std::min<uint64_t>(
           {(Q0 + zk::kDQuads - 1) / zk::kDQuads, (uint64_t)std::min<uint32_t>(c->dtail_blocks, 64u), (uint64_t)c->num_cus});
       double bytes = 0, muls = 0;
@@ -949,6 +1023,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   auto hand_on = [&](size_t si) {
     if (!pre || si + 1 >= ns) return;
     const GStep& nx = steps[si + 1];
+    if (nx.kind == GS_HOST) return;
     if (nx.kind == GS_T32 || nx.kind == GS_T33 || nx.kind == GS_TT || nx.kind == GS_TTAIL) {
       post.post2(rz, ra, rb, rtags[si + 1]);
     } else if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
@@ -998,12 +1073,15 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     one_round(i0 + 1, V[0], hfe_sub<F>(claim, V[0]), at2w(V[0], V[1], V[2]));
     Fe wb[3];
     wts(r, wb);
-    Fe Z[3];  // round i0 + 2: Z[gamma] = sum w(ra, alpha) w(rb, beta) T
+    Fe Z[3];  // round i0 + 2: Z[gamma] = sum_alpha w(ra, alpha) sum_beta w(rb, beta) T
     for (int g = 0; g < 3; ++g) {
-      Z[g] = fe_zero<F>();
-      for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b)
-          Z[g] = hfe_add<F>(Z[g], hfe_mul<F>(hfe_mul<F>(wa[a], wb[b]), T[9 * a + 3 * b + g]));
+      uint64_t acc[9] = {0};
+      for (int a = 0; a < 3; ++a) {
+        uint64_t in[9] = {0};
+        for (int b = 0; b < 3; ++b) h64::mac_wide(in, h64::of(wb[b]), h64::of(T[9 * a + 3 * b + g]));
+        h64::mac_wide(acc, h64::of(wa[a]), h64::of(wide_to_fe<F>(in)));
+      }
+      Z[g] = wide_to_fe<F>(acc);
     }
     one_round(i0 + 2, Z[0], hfe_sub<F>(claim, Z[0]), at2w(Z[0], Z[1], Z[2]));
   };
@@ -1077,6 +1155,34 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     } else if (st.kind == GS_DOUBLE) {
       two_rounds(st.i);
       pend = 2;
+    } else if (st.kind == GS_HOST) {
+      // the previous (persistent tail) step's output: level i - 2, 4 tables of
+      // 2^(H+2) in h_tab, complete once its flag was seen; fold by r_{i-2}, r_{i-1}
+      const auto t0 = std::chrono::steady_clock::now();
+      const size_t len = (size_t)1 << (nv - st.i + 2);
+      std::vector<Fe> T[4];
+      for (int t = 0; t < 4; ++t) {  // word-major per table (kernels.hpp st_fe_sys)
+        const uint64_t* w = c->h_tab + (size_t)t * 4 * len;
+        T[t].resize(len);
+        for (size_t e = 0; e < len; ++e)
+          for (int k = 0; k < 4; ++k) {
+            const uint64_t x = w[k * len + e];
+            T[t][e].v[2 * k] = (uint32_t)x;
+            T[t][e].v[2 * k + 1] = (uint32_t)(x >> 32);
+          }
+      }
+      host_fold<F>(T, ra);
+      host_fold<F>(T, rb);
+      for (uint32_t i = st.i; i < nv; ++i) {
+        Fe e0, e2;
+        host_round_sums<F>(T, e0, e2);
+        one_round(i, e0, zk::hfe_sub<F>(claim, e0), e2);
+        if (i + 1 < nv) host_fold<F>(T, r);
+      }
+      if (c->tail_trace)
+        fprintf(stderr, "zk host rounds %u..%u: %.2f us\n", st.i, nv - 1,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+      pend = 0;
     } else {  // GS_DTAIL
       for (uint32_t d = 0; d < st.nd; ++d) {
         two_rounds(st.i + 2 * d);
@@ -1092,7 +1198,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint64_t* T = c->tail_trace + 512;
     uint64_t prev_pub = 0;
     for (size_t si = 0; si < ns; ++si) {
-      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL) break;
+      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL || steps[si].kind == GS_HOST) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
       const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T;  // no challenge to wait for
       const uint64_t rr = first ? row[0] : row[1];
@@ -1160,10 +1266,11 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
               (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, (T[m * 8 + 5] - T[m * 8 + 4]) * 0.01,
               m + 1 < nd ? (T[m * 8 + 9] - T[m * 8 + 5]) * 0.01 : 0.0);
   }
-  if (c->tail_trace && !steps.empty() && steps.back().kind == GS_DTAIL) {  // ZK_DEBUG_TAIL
+  const size_t sdt = !steps.empty() && steps.back().kind == GS_HOST ? steps.size() - 2 : steps.size() - 1;
+  if (c->tail_trace && !steps.empty() && steps[sdt].kind == GS_DTAIL) {  // ZK_DEBUG_TAIL
     HIPCK(hipStreamSynchronize(c->stream));
     const uint64_t* T = c->tail_trace;
-    const uint32_t nd = steps.back().nd;
+    const uint32_t nd = steps[sdt].nd;
     for (uint32_t m = 0; m < nd; ++m)
       fprintf(stderr, "zk dtail step %u: wait r %6.2f us, fold+eval %6.2f, limb sums %6.2f, fan-in %6.2f, publish %6.2f, hand-off to next r %6.2f\n",
               m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
@@ -1191,7 +1298,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   const Fe* cur[4] = {dT[0], dT[1], dT[2], dT[3]};
   Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
   uint32_t pend = 0;
-  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend);
+  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend, lg == 0);  // one rank: the final tables are not needed
   if (lg == 0) {
     sync(c);  // settles event timings; the results are already on the host
     return;

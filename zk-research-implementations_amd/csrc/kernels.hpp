@@ -22,6 +22,16 @@ __device__ __forceinline__ Fe ld_fe(const Fe* __restrict__ p, uint64_t i) {
   r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
   return r;
 }
+// streaming (nt) load: read-once inputs (experiment knob ZK_T33_NTL, compile time)
+__device__ __forceinline__ Fe ld_fe_nt(const Fe* __restrict__ p, uint64_t i) {
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t* q = reinterpret_cast<const u32x4_t*>(p) + 2 * i;
+  const u32x4_t a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+  Fe r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
 __device__ __forceinline__ void st_fe(Fe* __restrict__ p, uint64_t i, const Fe& x) {
   uint4* q = reinterpret_cast<uint4*>(p) + 2 * i;
   q[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
@@ -1195,11 +1205,26 @@ struct DTailArgs {
   RPost* relay;       // nsteps fresh relay slots
   uint32_t* err;      // pinned error word
   uint64_t* trace;    // debug (ZK_DEBUG_TAIL): per step 8 s_memrealtime stamps, or null
+  uint64_t* host_tab; // pinned host memory: the last step's 4 output tables (16 Q elements), or null (host-side rounds)
 };
 __host__ __device__ __forceinline__ uint64_t dtail_region(uint64_t Q0, uint32_t s) {
   uint64_t o = 0;
   for (uint32_t t = 0; t < s; ++t) o += 16 * (Q0 >> (2 * t));
   return o;
+}
+
+// The last device step (host_tab set) stores its output tables to pinned host
+// memory instead, with system-scope stores, word-major per table (word k of
+// element i at k n + i: one store instruction writes 512 contiguous bytes —
+// element-major 8-byte stores crossed the host link one by one, ~20 ns each);
+// every storing wave drains (vmcnt(0)) before its block counts in, so the flag
+// the last block raises comes after every table store has completed: the host
+// runs the remaining rounds on them (host.hpp "host rounds").
+__device__ __forceinline__ void st_fe_sys(uint64_t* p, uint64_t n, uint64_t i, const Fe& x) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    __hip_atomic_store(p + k * n + i, (uint64_t)x.v[2 * k] | ((uint64_t)x.v[2 * k + 1] << 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <class F>
@@ -1234,6 +1259,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
       X = prev + (uint64_t)tb * 16 * Q;
     }
     Fe* X2 = a.out + dtail_region(a.Q0, st) + (uint64_t)tb * 4 * Q;
+    uint64_t* H2 = a.host_tab && st + 1 == a.nsteps ? a.host_tab + (uint64_t)tb * 16 * Q : nullptr;
     Wide acc = wide_zero<F>();
     for (uint64_t jb = (uint64_t)blockIdx.x * kDQuads; jb < Q; jb += (uint64_t)nb * kDQuads) {
       const uint64_t j = jb + jl;
@@ -1241,7 +1267,10 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
         const uint64_t i = j + k * Q;
         const Fe z = two ? fold2c<F>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ld_fe_a(X, i + 2 * h4), ld_fe_a(X, i + 3 * h4), ct)
                          : fold1c<F, 1>(ld_fe_a(X, i), ld_fe_a(X, i + h4), ct);
-        st_fe_a(X2, i, z);
+        if (H2)
+          st_fe_sys(H2, 4 * Q, i, z);
+        else
+          st_fe_a(X2, i, z);
         unit_product<F>(z, k, tab, acc);
       }
     }

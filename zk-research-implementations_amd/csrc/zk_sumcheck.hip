@@ -56,6 +56,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_DTAIL_MAX_QUADS")) c->dtail_max_quads = strtoull(e, nullptr, 0);
     if (const char* e = getenv("ZK_ATOMIC_FANIN")) c->atomic_fanin = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_DTAIL_BLOCKS")) c->dtail_blocks = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char* e = getenv("ZK_HOST_ROUNDS")) c->host_rounds = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_TAIL_MAX_PAIRS")) c->tail_max_pairs = strtoull(e, nullptr, 0);
     c->num_cus = prop.multiProcessorCount;
     try {
@@ -105,6 +106,7 @@ void zk_ctx_destroy(zk_ctx* c) {
   for (auto& b : c->scan_tmp) b.release();
   c->g1_table.release();
   if (c->h_red) (void)hipHostFree(c->h_red);
+  if (c->h_tab) (void)hipHostFree(c->h_tab);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
