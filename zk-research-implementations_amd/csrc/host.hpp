@@ -213,6 +213,7 @@ struct zk_ctx {
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
+  uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
   size_t h_tab_bytes = 0;
@@ -856,7 +857,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (st.kind == GS_T33) {  // rounds i .. i+2 over level i's octants: 27 moment sums
         const uint64_t O = size / 8;
         // 64-octant chunks while they still give every CU a chunk, else 32 (twice the blocks)
-        if (O / 64 >= (uint64_t)c->num_cus) {
+        if (O / 64 >= (uint64_t)c->num_cus * c->t33_oct64_min) {
           const uint64_t nch = O / 64;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64>);
           const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);

@@ -22,16 +22,6 @@ __device__ __forceinline__ Fe ld_fe(const Fe* __restrict__ p, uint64_t i) {
   r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
   return r;
 }
-// streaming (nt) load: read-once inputs (experiment knob ZK_T33_NTL, compile time)
-__device__ __forceinline__ Fe ld_fe_nt(const Fe* __restrict__ p, uint64_t i) {
-  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-  const u32x4_t* q = reinterpret_cast<const u32x4_t*>(p) + 2 * i;
-  const u32x4_t a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
-  Fe r;
-  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
-  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
-  return r;
-}
 __device__ __forceinline__ void st_fe(Fe* __restrict__ p, uint64_t i, const Fe& x) {
   uint4* q = reinterpret_cast<uint4*>(p) + 2 * i;
   q[0] = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);

@@ -29,10 +29,6 @@
 #pragma once
 #include "kernels.hpp"
 
-#ifndef ZK_T33_NTL
-#define ZK_T33_NTL 0  // k_gkr_t33 input loads: 1 = streaming (nt)
-#endif
-
 namespace zk {
 
 typedef int i32x2 __attribute__((ext_vector_type(2)));
@@ -895,7 +891,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   auto in_at = [&](uint64_t ch, int f, Fe (&x)[8]) {
     const uint64_t e = OCT == 64 ? ch * 64 + l + (uint64_t)f * O : ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = ZK_T33_NTL ? ld_fe_nt(X, e + k * h8) : ld_fe(X, e + k * h8);
+    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
   };
   // inputs two folds ahead (one wave per SIMD: the loads in flight are what
   // hides HBM latency). OCT 64: the first two folds' inputs (written by the
