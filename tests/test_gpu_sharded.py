@@ -80,6 +80,51 @@ def _steps(nloc: int, d0: bool = True) -> int:
     return 2 + (nloc - 2) % 2 + (nloc - 2) // 2
 
 
+def _bounds(nloc: int, d0: bool = True) -> list[int]:
+    """End round of each step of a sharded phase (no persistent steps across
+    ranks), as host.hpp gkr_phase builds the schedule."""
+    b: list[int] = []
+    if nloc == 0:
+        return b
+    if d0 and nloc >= 11:
+        nt, k = -1, 0
+        while 3 + 3 * k + 8 <= nloc:
+            r = nloc - 3 - 3 * k
+            if r % 2 == 0 and (r >= 12 or nt < 0):
+                nt = k
+            k += 1
+        b = [3 + 3 * k for k in range(nt + 1)] + [5 + 3 * nt]
+        i = 5 + 3 * nt
+    elif d0 and nloc >= 2 and nloc % 2 == 0:
+        b, i = [2], 2
+    else:
+        b, i = [1], 1
+        if nloc >= 2:
+            i += 1
+            b.append(i)
+        if nloc >= 3 and (nloc - 2) % 2 == 1:
+            i += 1
+            b.append(i)
+    while i + 1 < nloc:
+        i += 2
+        b.append(i)
+    return b
+
+
+def _collectives(nloc: int, gather_vars: int = 10, d0: bool = True) -> int:
+    """All-reduces of a sharded proof (world > 1): one per step until the
+    first step boundary leaving <= gather_vars local rounds, then ONE gather
+    of the folded tables (host.hpp gkr_prove_device); every later round runs
+    locally on every rank. Without such a boundary: every step + the final
+    gather of one element per table."""
+    b = _bounds(nloc, d0)
+    if gather_vars > 0:
+        for s, e in enumerate(b):
+            if e < nloc and nloc - e <= gather_vars:
+                return s + 1 + 1
+    return len(b) + 1
+
+
 # (2, 20, 0): each rank's first kernel fills the card (512 blocks) while the
 # other rank shares it: with pre-enqueued kernels spinning on their challenges
 # this starved the other rank; the library launches step by step under a host
@@ -93,7 +138,7 @@ def test_host_comm_ranks_match_single_process(tmp_path, world, nloc, field):
         assert {"polys": r["polys"], "chal": r["chal"]} == {"polys": want["polys"], "chal": want["chal"]}, f"rank {rank}"
         # f4: the whole proof as one digest, identical on every rank and to the CPU oracle's
         assert r["blob_keccak"] == want["blob_keccak"], f"rank {rank}"
-        assert r["collectives"] == _steps(nloc) + 1  # one all-reduce per step + the tail gather
+        assert r["collectives"] == _collectives(nloc)  # one all-reduce per step until the gather, then the gather
 
 
 def test_world1_without_comm(tmp_path):
@@ -121,4 +166,19 @@ def test_first_double_step_sharded(tmp_path, comm, world, nloc):
     want = _oracle(0, nloc + world.bit_length() - 1)
     for rank, r in enumerate(res):
         assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
-        assert r["collectives"] == _steps(nloc, d0=True) + (1 if world > 1 else 0)
+        assert r["collectives"] == (_collectives(nloc) if world > 1 else _steps(nloc, d0=True))
+
+
+@pytest.mark.parametrize("world,nloc,field,gather", [(2, 16, 0, "0"), (2, 16, 2, "4"), (4, 13, 1, "6"), (2, 20, 0, "10"),
+                                                     (2, 12, 0, "20")])
+def test_early_gather_matches_single_process(tmp_path, world, nloc, field, gather):
+    """ZK_GATHER_VARS: the ranks stop at the first step boundary leaving <= this
+    many local rounds, fold by the pending challenges, gather every rank's
+    tables with one all-reduce of a one-hot buffer, and finish the proof
+    locally (0: run every local round, then gather one element per table).
+    Every setting gives every rank the single-process oracle's proof."""
+    res = _run(world, "host", field, nloc, str(tmp_path), {"ZK_GATHER_VARS": gather})
+    want = _oracle(field, nloc + world.bit_length() - 1)
+    for rank, r in enumerate(res):
+        assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
+        assert r["collectives"] == _collectives(nloc, int(gather)), f"rank {rank}"

@@ -1,4 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-ZK_T33_OCT64_MIN=4 bash tools/gpu_trace.sh | grep "zk step [0-4]"
-REPS="1 2 3 4" bash tools/gpu_ab_env.sh ZK_T33_OCT64_MIN=1 ZK_T33_OCT64_MIN=4
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 900 python -u -m pytest tests/test_gpu_sharded.py -x -v --timeout 280 --timeout-method thread > gpurun_out/pytest_sharded.log 2>&1 || { grep -E "PASS|FAIL|Error|error" gpurun_out/pytest_sharded.log | tail -30; exit 1; }
+grep -cE "PASSED" gpurun_out/pytest_sharded.log; tail -1 gpurun_out/pytest_sharded.log
+bash tools/gpu_rehearsal.sh

@@ -213,6 +213,8 @@ struct zk_ctx {
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
   uint64_t dtail_max_quads = 1u << 10;  // it starts at the first double step with <= this many quads (ZK_DTAIL_MAX_QUADS)
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
+  uint32_t gather_vars = 10;  // sharded: gather the tables once <= this many local rounds remain, finish locally (ZK_GATHER_VARS; 0: at the end)
+  DevBuf gbuf;                // sharded gather: fold scratch, the one-hot buffer, the interleaved global tables
   uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
@@ -587,9 +589,12 @@ void host_round_sums(const std::vector<Fe> (&T)[4], Fe& e0, Fe& e2) {
   e2 = wide_to_fe<F>(a2);
 }
 
+// gather_max > 0 (sharded phases): stop after the first step boundary b with
+// nv - b <= gather_max; *stop = b (nv when the phase runs to its end).
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
-               GkrOut& out, Fe& claim, Fe& r, uint32_t& pend, bool host_ok = false) {
+               GkrOut& out, Fe& claim, Fe& r, uint32_t& pend, bool host_ok = false, uint32_t gather_max = 0,
+               uint32_t* stop = nullptr) {
   const uint64_t L = (uint64_t)1 << nv;
   const bool pre = prelaunch(c, nv);
   std::vector<GStep> steps;
@@ -722,23 +727,38 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       steps.push_back({GS_SINGLE, i, 0});
     }
   }
+  auto rounds_of = [&](const GStep& st) -> uint32_t {
+    switch (st.kind) {
+      case GS_DOUBLE: case GS_D0: case GS_T32: return 2;
+      case GS_D0T: case GS_T33: case GS_TT: return 3;
+      case GS_DTAIL: return 2 * st.nd;
+      case GS_TTAIL: return 3 * st.nd;
+      case GS_TAIL: case GS_HOST: return nv - st.i;
+      default: return 1;
+    }
+  };
+  uint32_t end = nv;  // rounds this phase runs
+  if (gather_max > 0) {  // sharded: stop at the first boundary leaving <= gather_max rounds (host.hpp gkr_prove_device)
+    for (size_t s = 0; s < steps.size(); ++s) {
+      const uint32_t b = steps[s].i + rounds_of(steps[s]);
+      const int k = steps[s].kind;
+      if (k == GS_TAIL || k == GS_DTAIL || k == GS_TTAIL || k == GS_HOST) break;  // (persistent steps are not cut)
+      if (b < nv && nv - b <= gather_max) {
+        steps.resize(s + 1);
+        end = b;
+        break;
+      }
+    }
+  }
+  if (stop) *stop = end;
   const size_t ns = steps.size();
-  {  // the schedule covers rounds 0 .. nv-1 exactly once, in order (checked before anything launches)
+  {  // the schedule covers rounds 0 .. end-1 exactly once, in order (checked before anything launches)
     uint32_t next = 0;
     for (const GStep& st : steps) {
-      uint32_t nr = 1;
-      switch (st.kind) {
-        case GS_DOUBLE: case GS_D0: case GS_T32: nr = 2; break;
-        case GS_D0T: case GS_T33: case GS_TT: nr = 3; break;
-        case GS_DTAIL: nr = 2 * st.nd; break;
-        case GS_TTAIL: nr = 3 * st.nd; break;
-        case GS_TAIL: case GS_HOST: nr = nv - st.i; break;
-        default: nr = 1;
-      }
       if (st.i != next) fail(ZK_EINVAL, "internal: step schedule out of order");
-      next += nr;
+      next += rounds_of(st);
     }
-    if (next != nv) fail(ZK_EINVAL, "internal: step schedule does not cover every round");
+    if (next != end) fail(ZK_EINVAL, "internal: step schedule does not cover every round");
   }
   std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
   std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
@@ -1299,9 +1319,60 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   const Fe* cur[4] = {dT[0], dT[1], dT[2], dT[3]};
   Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
   uint32_t pend = 0;
-  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend, lg == 0);  // one rank: the final tables are not needed
+  uint32_t stop = nloc;
+  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend, lg == 0,  // one rank: the final tables are not needed
+               lg > 0 ? c->gather_vars : 0, &stop);
   if (lg == 0) {
     sync(c);  // settles event timings; the results are already on the host
+    return;
+  }
+  if (stop < nloc) {
+    // ---- early gather: T = nloc - stop local rounds remain. Every rank folds
+    // its tables by the pending challenges (r_{stop-pend} .. r_{stop-1}) to 4 x
+    // 2^T, writes them into its slot of a zeroed one-hot buffer [G][4][2^T]
+    // (exact under a u64 SUM: every word has one nonzero contributor), one
+    // all-reduce gathers every rank's slot, k_interleave lays out the global
+    // tables (index m G + g), and every rank runs the last T + lg rounds
+    // locally, with no further collective: the small steps, whose latency an
+    // all-reduce per step would dominate, run in the persistent tail and on
+    // the host exactly as for one GPU. Same rounds, same transcript.
+    const uint32_t T = nloc - stop;
+    const uint64_t Tn = (uint64_t)1 << T;
+    const uint64_t sz = (uint64_t)1 << (T + pend);  // current table length
+    const size_t scratch = (size_t)4 * sz, onehot = (size_t)G * 4 * Tn, global = (size_t)4 * G * Tn;
+    c->gbuf.ensure((scratch + onehot + global) * sizeof(Fe));
+    Fe* sc = reinterpret_cast<Fe*>(c->gbuf.p);
+    Fe* oh = sc + scratch;
+    Fe* gl = oh + onehot;
+    HIPCK(hipMemsetAsync(oh, 0, onehot * sizeof(Fe), c->stream));
+    Fe* slot = oh + (size_t)c->rank * 4 * Tn;
+    if (pend == 0) {
+      for (int t = 0; t < 4; ++t) HIPCK(hipMemcpyAsync(slot + t * Tn, cur[t], Tn * 32, hipMemcpyDeviceToDevice, c->stream));
+    }
+    for (uint32_t j = 0; j < pend; ++j) {
+      const uint64_t half = sz >> (j + 1);
+      Fe* dst = j + 1 == pend ? slot : sc + (j & 1 ? 2 * sz : 0);  // (scratch halves alternate; the last fold lands in the slot)
+      const uint64_t dstride = j + 1 == pend ? Tn : half;
+      const Fe& rj = out.challenges[stop - pend + j];
+      launch(c, ZK_K_FOLD, 4 * half * 96.0, 4.0 * half, zk::k_fold4<F>, grid_for(c, half, zk::k_fold4<F>), cur[0], cur[1],
+             cur[2], cur[3], dst, dst + dstride, dst + 2 * dstride, dst + 3 * dstride, half, rj);
+      for (int t = 0; t < 4; ++t) cur[t] = dst + t * dstride;
+    }
+    if (c->comm == COMM_RCCL) {
+      NCCLCK(ncclAllReduce(oh, oh, onehot * 4, ncclUint64, ncclSum, c->nccl, c->stream));
+      c->stats.collectives += 1;
+    } else {
+      std::vector<uint64_t> w(onehot * 4);
+      HIPCK(hipMemcpyAsync(w.data(), oh, onehot * sizeof(Fe), hipMemcpyDeviceToHost, c->stream));
+      sync(c);
+      allreduce_host(c, w.data(), w.size());
+      HIPCK(hipMemcpyAsync(oh, w.data(), onehot * sizeof(Fe), hipMemcpyHostToDevice, c->stream));
+    }
+    launch(c, ZK_K_FOLD, global * 64.0, 0.0, zk::k_interleave<F>, grid_for(c, global, zk::k_interleave<F>), (const Fe*)oh, gl,
+           Tn, (uint32_t)G);
+    const Fe* gcur[4] = {gl, gl + G * Tn, gl + 2 * G * Tn, gl + 3 * G * Tn};
+    gkr_phase<F>(c, gcur, T + lg, stop, false, tr, out, claim, r, pend, true);
+    sync(c);
     return;
   }
 

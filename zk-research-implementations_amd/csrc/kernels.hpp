@@ -1347,6 +1347,19 @@ __global__ __launch_bounds__(kBlock) void k_fold(const Fe* __restrict__ X, Fe* _
   }
 }
 
+// Sharded proofs, after the gather (host.hpp gkr_prove_device): the one-hot
+// buffer holds rank g's 4 tables of T elements at [g][table][m]; the global
+// table t is indexed m G + g (rank g owns the low index bits g).
+template <class F>
+__global__ __launch_bounds__(kBlock) void k_interleave(const Fe* __restrict__ in, Fe* __restrict__ out, uint64_t T,
+                                                      uint32_t G) {
+  const uint64_t n = 4 * (uint64_t)G * T, stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t o = (uint64_t)blockIdx.x * kBlock + threadIdx.x; o < n; o += stride) {
+    const uint64_t t = o / (G * T), rem = o % (G * T), m = rem / G, g = rem % G;
+    st_fe(out, o, ld_fe(in, (g * 4 + t) * T + m));
+  }
+}
+
 // fold four tables by r at bit 0 (used before the multi-GPU all-gather)
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_fold4(const Fe* __restrict__ A, const Fe* __restrict__ S,

@@ -56,6 +56,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_DTAIL_MAX_QUADS")) c->dtail_max_quads = strtoull(e, nullptr, 0);
     if (const char* e = getenv("ZK_ATOMIC_FANIN")) c->atomic_fanin = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_DTAIL_BLOCKS")) c->dtail_blocks = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char* e = getenv("ZK_GATHER_VARS")) c->gather_vars = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_T33_OCT64_MIN")) c->t33_oct64_min = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_HOST_ROUNDS")) c->host_rounds = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_TAIL_MAX_PAIRS")) c->tail_max_pairs = strtoull(e, nullptr, 0);
@@ -103,6 +104,7 @@ void zk_ctx_destroy(zk_ctx* c) {
   if (c->tail_trace) (void)hipHostFree(c->tail_trace);
   if (c->block_trace) (void)hipHostFree(c->block_trace);
   c->small.release();
+  c->gbuf.release();
   for (auto& b : c->msm) b.release();
   for (auto& b : c->scan_tmp) b.release();
   c->g1_table.release();
