@@ -1181,9 +1181,14 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       // 2^(H+2) in h_tab, complete once its flag was seen; fold by r_{i-2}, r_{i-1}
       const auto t0 = std::chrono::steady_clock::now();
       const size_t len = (size_t)1 << (nv - st.i + 2);
+      // one bulk copy first: the device wrote these lines, so every host read
+      // misses; memcpy keeps many misses in flight, the unpack then hits L1
+      std::vector<uint64_t> raw((size_t)16 * len);
+      memcpy(raw.data(), c->h_tab, raw.size() * 8);
+      const auto t1 = std::chrono::steady_clock::now();
       std::vector<Fe> T[4];
       for (int t = 0; t < 4; ++t) {  // word-major per table (kernels.hpp st_fe_sys)
-        const uint64_t* w = c->h_tab + (size_t)t * 4 * len;
+        const uint64_t* w = raw.data() + (size_t)t * 4 * len;
         T[t].resize(len);
         for (size_t e = 0; e < len; ++e)
           for (int k = 0; k < 4; ++k) {
@@ -1201,8 +1206,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         if (i + 1 < nv) host_fold<F>(T, r);
       }
       if (c->tail_trace)
-        fprintf(stderr, "zk host rounds %u..%u: %.2f us\n", st.i, nv - 1,
-                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        fprintf(stderr, "zk host rounds %u..%u: %.2f us (table copy %.2f us)\n", st.i, nv - 1,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(),
+                std::chrono::duration<double, std::micro>(t1 - t0).count());
       pend = 0;
     } else {  // GS_DTAIL
       for (uint32_t d = 0; d < st.nd; ++d) {
