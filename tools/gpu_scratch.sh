@@ -1,5 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_prelaunch.py -x -q --timeout 120 --timeout-method thread -k "host_rounds" > gpurun_out/p.log 2>&1 || { tail -30 gpurun_out/p.log; exit 1; }
-tail -1 gpurun_out/p.log
-bash tools/gpu_trace.sh | grep "host rounds\|flag -> post" | tail -12
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sharded.py -x -q --timeout 280 --timeout-method thread > gpurun_out/ps.log 2>&1 || { tail -30 gpurun_out/ps.log; exit 1; }
+tail -1 gpurun_out/ps.log
+ZK_HOST_ROUNDS=6 bash tools/gpu_trace.sh | grep "host rounds" | tail -2
+REPS="1 2 3 4 5" bash tools/gpu_ab_env.sh ZK_HOST_ROUNDS=4 ZK_HOST_ROUNDS=6

@@ -1373,6 +1373,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
       sync(c);
       allreduce_host(c, w.data(), w.size());
       HIPCK(hipMemcpyAsync(oh, w.data(), onehot * sizeof(Fe), hipMemcpyHostToDevice, c->stream));
+      sync(c);  // w (pageable) is released at the end of this block
     }
     launch(c, ZK_K_FOLD, global * 64.0, 0.0, zk::k_interleave<F>, grid_for(c, global, zk::k_interleave<F>), (const Fe*)oh, gl,
            Tn, (uint32_t)G);
