@@ -1,6 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_prelaunch.py tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread > gpurun_out/p.log 2>&1 || { tail -30 gpurun_out/p.log; exit 1; }
-tail -1 gpurun_out/p.log
-bash tools/gpu_trace.sh | grep -v "flag -> post" | tail -8
-REPS="1 2 3 4 5" bash tools/gpu_ab_env.sh ZK_DTAIL3=0 ZK_DTAIL3=1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+bash tools/ab_libs.sh abtest/old.so
+ZK_LIB_PATH=abtest/old.so bash tools/gpu_trace.sh | grep "zk step 1 "
+bash tools/gpu_trace.sh | grep "zk step 1 "

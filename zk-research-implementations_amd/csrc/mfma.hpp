@@ -285,6 +285,33 @@ __device__ __forceinline__ Fe sub256(const Fe& a, const Fe& b) {  // two's compl
 __device__ __forceinline__ int64_t word_of(int a0, int a1, int a2, int a3) {
   return (int64_t)a0 + ((int64_t)a1 << 8) + ((int64_t)a2 << 16) + ((int64_t)a3 << 24);
 }
+// The two B fragments of a fold MFMA pair straight from one v_permlane32_swap
+// per register pair (no selects): with vdst = word q (bytes 4q..) and vsrc =
+// word 4 + q of the lane's element, the swapped vdst holds [word q of elements
+// 0..31 | word 4 + q of elements 0..31] (acc0's columns), the swapped vsrc
+// [word q of elements 32..63 | word 4 + q of elements 32..63] (acc1's).
+__device__ __forceinline__ void fold_operands(const Fe& x, i32x4& b0, i32x4& b1) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x.v[q], x.v[4 + q], false, false);
+    b0[q] = (int)r[0];
+    b1[q] = (int)r[1];
+  }
+}
+// The result words after a fold MFMA pair: lane (e, h) holds words 2g + h of
+// both columns (acc0: element e, acc1: element 32 + e); one swap per 32-bit
+// half gives every lane words 2g and 2g + 1 of its own element.
+__device__ __forceinline__ void fold_words(const i32x16& acc0, const i32x16& acc1, int64_t (&W)[8]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const uint64_t w0 = (uint64_t)word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
+    const uint64_t w1 = (uint64_t)word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)w0, (uint32_t)w1, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(w0 >> 32), (uint32_t)(w1 >> 32), false, false);
+    W[2 * g] = (int64_t)(((uint64_t)hi[0] << 32) | lo[0]);
+    W[2 * g + 1] = (int64_t)(((uint64_t)hi[1] << 32) | lo[1]);
+  }
+}
 
 // Z = x00 + Y 2^-64 (mod p), Y = sum_i W[i] 2^(32 i) (signed words, |Y| < 2^271)
 template <class F>
@@ -358,7 +385,6 @@ __device__ __forceinline__ Fe dm_fold(const Fe (&x)[4], const i32x4 (&wf)[3]) {
     d[1] = fe_sub<F>(x01, x00);
     d[2] = fe_sub<F>(fe_sub<F>(x11, x01), d[0]);
   }
-  const bool h = (threadIdx.x & 32) != 0;
   i32x16 acc0, acc1;  // columns: elements j0 .. j0+31 (acc0), j0+32 .. j0+63 (acc1)
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0;
@@ -366,31 +392,14 @@ __device__ __forceinline__ Fe dm_fold(const Fe (&x)[4], const i32x4 (&wf)[3]) {
   for (int c = 0; c < 3; ++c) {
     to_digits(d[c]);
     // B fragment of lane (e, h): digits 16h .. 16h+15 of element e (acc0) / 32 + e (acc1);
-    // lane e owns element e, lane e + 32 element 32 + e: trade the half the partner needs
-    i32x4 own_lo, own_hi, got;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      own_lo[q] = (int)d[c].v[q];
-      own_hi[q] = (int)d[c].v[4 + q];
-      got[q] = (int)xchg32(h ? d[c].v[q] : d[c].v[4 + q]);
-    }
-    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? got : own_lo, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? own_hi : got, acc1, 0, 0, 0);
+    // lane e owns element e, lane e + 32 element 32 + e (fold_operands)
+    i32x4 b0, b1;
+    fold_operands(d[c], b0, b1);
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], b0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], b1, acc1, 0, 0, 0);
   }
-  // lane (e, h) holds words 2g + h (g = 0..3) of both columns; it keeps its own element's
-  // (acc0 for h = 0, acc1 for h = 1) and sends the partner's
   int64_t W[8];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int64_t keep = h ? word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3])
-                           : word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
-    const int64_t send = h ? word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3])
-                           : word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
-    const uint32_t lo = xchg32((uint32_t)send), hi = xchg32((uint32_t)((uint64_t)send >> 32));
-    const int64_t recv = (int64_t)(((uint64_t)hi << 32) | lo);
-    W[2 * g] = h ? recv : keep;
-    W[2 * g + 1] = h ? keep : recv;
-  }
+  fold_words(acc0, acc1, W);
   return dm_finish<F>(W, x00);
 }
 
@@ -759,35 +768,19 @@ struct DM3Scratch : DMScratch {
 };
 template <class F, int NP = 3>
 __device__ __forceinline__ Fe dm3_fold(Fe (&x)[1 << NP], const i32x4 (&wf)[1 << NP]) {
-  const bool h = (threadIdx.x & 32) != 0;
   i32x16 acc0, acc1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0;
 #pragma unroll
   for (int c = 0; c < (1 << NP); ++c) {
     to_digits(x[c]);
-    i32x4 own_lo, own_hi, got;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      own_lo[q] = (int)x[c].v[q];
-      own_hi[q] = (int)x[c].v[4 + q];
-      got[q] = (int)xchg32(h ? x[c].v[q] : x[c].v[4 + q]);
-    }
-    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? got : own_lo, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], h ? own_hi : got, acc1, 0, 0, 0);
+    i32x4 b0, b1;
+    fold_operands(x[c], b0, b1);
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], b0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], b1, acc1, 0, 0, 0);
   }
   int64_t W[8];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int64_t keep = h ? word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3])
-                           : word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3]);
-    const int64_t send = h ? word_of(acc0[4 * g], acc0[4 * g + 1], acc0[4 * g + 2], acc0[4 * g + 3])
-                           : word_of(acc1[4 * g], acc1[4 * g + 1], acc1[4 * g + 2], acc1[4 * g + 3]);
-    const uint32_t lo = xchg32((uint32_t)send), hi = xchg32((uint32_t)((uint64_t)send >> 32));
-    const int64_t recv = (int64_t)(((uint64_t)hi << 32) | lo);
-    W[2 * g] = h ? recv : keep;
-    W[2 * g + 1] = h ? keep : recv;
-  }
+  fold_words(acc0, acc1, W);
   return dm_finish<F>(W, fe_zero<F>());
 }
 
