@@ -56,6 +56,36 @@ def parse():
     return ap.parse_args()
 
 
+def golden_key(field: int, n: int, seed: int) -> str:
+    return f"{[k for k, v in FIELDS.items() if v == field][0]}_{n}_s{seed}"
+
+
+def proof_check(field: int, n: int, seed: int, coeffs, nco, ch) -> dict:
+    """Keccak-256 of the proof blob (claimed sum = s_0(0) + s_0(1)), written
+    by the library's serialiser (zk_gkr_proof_to_blob), against the committed
+    full-size oracle fixture for this workload (tests/golden/large.json, from
+    oracle/zk_oracle.c or_gkr_prove_fast via tests/golden/make_large_golden.py)
+    when one exists. A mismatch aborts the bench: a wrong proof has no rate."""
+    import zk_amd
+    from zk_amd.elems import to_ints
+
+    polys = [to_ints(coeffs[k, : nco[k]]) for k in range(n)]
+    chal = to_ints(ch)
+    p = zk_amd.modulus(field)
+    c = polys[0] + [0] * (3 - len(polys[0]))
+    claimed = (2 * c[0] + c[1] + c[2]) % p
+    blob = zk_amd.GkrProof([zk_amd.UnivariatePoly(q, field) for q in polys], claimed, chal).to_bytes(field)
+    dig = zk_amd.keccak256(blob).hex()
+    key = golden_key(field, n, seed)
+    path = os.path.join(ROOT, "tests", "golden", "large.json")
+    fix = json.load(open(path)).get(key) if os.path.exists(path) else None
+    out = {"blob_keccak256": dig, "fixture": f"tests/golden/large.json[{key}]" if fix else None,
+           "matches_oracle_fixture": (dig == fix["blob_keccak256"]) if fix else None}
+    if fix and dig != fix["blob_keccak256"]:
+        raise SystemExit(f"proof digest {dig} != oracle fixture {fix['blob_keccak256']} ({key})")
+    return out
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -322,6 +352,7 @@ def config4_bench(ctx, field: int, world: int, rank: int, barrier, total_nvars: 
             times.append(time.perf_counter() - t0)
     for t in tabs:
         t.free()
+    digest = proof_check(field, total_nvars, 4, coeffs, nco, ch)
     times.sort()
     med = times[len(times) // 2]
     if world > 1:
@@ -334,6 +365,7 @@ def config4_bench(ctx, field: int, world: int, rank: int, barrier, total_nvars: 
         "ms_median": med * 1e3,
         "field_ops_per_s": 32.0 * ((1 << total_nvars) - 1) / med,
         "challenge0_lo": int(ch[0, 0]),
+        "proof": digest,
     }
 
 
@@ -406,6 +438,8 @@ def main() -> None:
         if world > 1:
             dist.barrier()
 
+    step()  # the first proof, checked against the full-size oracle fixture
+    digest = proof_check(field, n, args.seed, coeffs, nco, ch)
     for _ in range(args.warmup):
         step()
     first_challenges = ch.copy()
@@ -509,6 +543,7 @@ def main() -> None:
                 + ("1 RCCL all-reduce of the step's limb sums (<= 243 x u64) per step of 2-3 rounds" if args.comm == "rccl" else
                    "host (gloo) all-reduce per round: diagnostic, not the product path") if world > 1 else "single GPU",
             },
+            "proof": digest,
             "roofline": {
                 "bound": "hbm",
                 "kernel": round_kinds.get(dom, dom) + "; the longest launch of the proof",

@@ -760,6 +760,10 @@ void or_synth_fill(int field, uint64_t seed, uint32_t table, uint64_t index0, ui
   const or_params* P = params(field);
   if (!P) return;
   uint64_t key = sm64(sm64(seed) + table);
+  /* counter-based: every element depends only on its index, so the parallel
+   * fill is identical to the serial one (the headline-size fixtures fill
+   * 4 x 2^26 elements) */
+#pragma omp parallel for schedule(static) if (count >= (1u << 16))
   for (uint64_t n = 0; n < count; ++n) {
     uint64_t i = index0 + n;
     uint64_t v[4];

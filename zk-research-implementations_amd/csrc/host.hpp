@@ -225,6 +225,7 @@ struct zk_ctx {
   uint64_t* tail_trace = nullptr;      // ZK_DEBUG_TAIL: pinned per-round stamps of the tail kernel, printed per proof
   uint64_t* block_trace = nullptr;     // ZK_DEBUG_BLOCKS=<step>: pinned per-block stamps of that step (needs ZK_DEBUG_TAIL)
   int block_trace_step = -1;
+  uint32_t grid_cap = 0;         // ZK_GRID_CAP: at most this many blocks for the grid-striding matrix-core steps (0: resident grid)
   uint32_t atomic_fanin = 1024;  // ZK_ATOMIC_FANIN: grids up to this many blocks fan in through u64 atomics
   uint32_t rtag = 0;        // last tag handed to a pre-enqueued round kernel
   void* user = nullptr;
@@ -281,6 +282,16 @@ uint32_t grid_for(zk_ctx* c, uint64_t work, K kernel) {
   uint64_t g = (work + zk::kBlock - 1) / zk::kBlock;
   if (g < 1) g = 1;
   return (uint32_t)std::min<uint64_t>(g, cap);
+}
+
+// Grid of a grid-striding matrix-core step: the resident grid `res`, capped
+// by ZK_GRID_CAP (tests: several chunks per block at oracle-checkable sizes),
+// but never below `min_blocks`, the count that keeps every block within its
+// int32 tile bound (k*ChunksMax in mfma.hpp).
+inline uint32_t step_grid(zk_ctx* c, uint32_t res, uint64_t min_blocks) {
+  uint64_t g = res;
+  if (c->grid_cap > 0 && g > c->grid_cap) g = c->grid_cap;
+  return (uint32_t)std::max<uint64_t>({g, min_blocks, 1});
 }
 
 // Launch wrapper: counts algorithmic bytes / multiplications per kernel kind
@@ -790,7 +801,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (c->d0 == 3) {  // products on the matrix cores (k_gkr_d0m, mfma.hpp)
         const uint64_t nch = (Q + 31) / 32;
         const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_d0m<F>);
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + 2 * zk::kD0MChunksMax - 1) / (2 * zk::kD0MChunksMax));
+        const uint32_t grid = step_grid(c, res, (nch + 2 * zk::kD0MChunksMax - 1) / (2 * zk::kD0MChunksMax));
         launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0m<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
       } else if (c->d0 == 2) {  // ZK_D0=2: the 8-lane k_gkr_d0 (DPP exchange, V11 in schoolbook rows)
         const uint32_t grid = grid_for(c, zk::kDQuads * Q, zk::k_gkr_d0<F>);
@@ -806,7 +817,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     if (st.kind == GS_D0T) {  // rounds 0, 1, 2 over the input tables (size 8 O), nothing written
       const uint64_t O = size / 8, nch = O / 32;
       const uint32_t res = grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F>) & ~1u;
-      const uint32_t grid = (uint32_t)std::max<uint64_t>({res, 2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax)});
+      const uint32_t grid = step_grid(c, res, std::max<uint64_t>(2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax))) & ~1u;
       launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
@@ -880,13 +891,13 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         if (O / 64 >= (uint64_t)c->num_cus * c->t33_oct64_min) {
           const uint64_t nch = O / 64;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64>);
-          const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
+          const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
           launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64>, grid, cur[0], cur[1], cur[2], cur[3],
                  nx[0], nx[1], nx[2], nx[3], O, din, sk);
         } else {
           const uint64_t nch = O / 32;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 32>);
-          const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kT33ChunksMax<32> - 1) / zk::kT33ChunksMax<32>);
+          const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<32> - 1) / zk::kT33ChunksMax<32>);
           launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 32>, grid, cur[0], cur[1], cur[2], cur[3],
                  nx[0], nx[1], nx[2], nx[3], O, din, sk);
         }
@@ -896,7 +907,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       }
       const uint64_t nch = Q / zk::kDMQuads;
       const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_dm3<F>);
-      const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
+      const uint32_t grid = step_grid(c, res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
       launch(c, ZK_K_GKR_DM, 4608.0 * Q, 48.0 * Q, zk::k_gkr_dm3<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0],
              nx[1], nx[2], nx[3], Q, din, sk);
       for (int t = 0; t < 4; ++t) cur[t] = nx[t];
@@ -982,7 +993,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (st.np == 2 && c->dm && Q >= std::max<uint64_t>(c->dm_min_quads, zk::kDMQuads)) {  // matrix cores (mfma.hpp)
         const uint64_t nch = Q / zk::kDMQuads;
         const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_dm<F>);
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
+        const uint32_t grid = step_grid(c, res, (nch + zk::kDMChunksMax - 1) / zk::kDMChunksMax);
         launch(c, ZK_K_GKR_DM, bytes, muls, zk::k_gkr_dm<F>, grid, cur[0], cur[1], cur[2], cur[3], nx[0], nx[1],
                nx[2], nx[3], Q, din, sk);
         for (int t = 0; t < 4; ++t) cur[t] = nx[t];

@@ -100,7 +100,8 @@ __device__ __forceinline__ void st_row(uint8_t* row, const Fe& x) {
 // Bounds: |C| <= 2^19 per chunk, so a wave takes at most kD0MChunksMax
 // chunks (int32 tiles); |G| < 2 * 2^16 * 2^510 < M < 2^530 for a block.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kD0MChunksMax = 2048;  // chunks of 32 quads per wave (int32 tile bound)
+constexpr uint32_t kD0MChunksMax = 2048;  // chunks of 32 quads per wave (int32 tile bound: 1 MFMA per chunk)
+static_assert(1ull * (1u << 19) * kD0MChunksMax <= (1ull << 30), "d0m tile bound");
 constexpr int kD0MPts = 5;                // point images per phase
 struct D0MScratch {
   uint8_t img[4][kD0MPts][2][32][32];   // per wave: point, table (X, Y), 32 rows of 32 bytes
@@ -404,7 +405,8 @@ __device__ __forceinline__ Fe dm_fold(const Fe (&x)[4], const i32x4 (&wf)[3]) {
 }
 
 constexpr uint32_t kDMQuads = 64;        // quads per chunk (one per lane)
-constexpr uint32_t kDMChunksMax = 1024;  // chunks per block (int32 product tiles: 2^20 per chunk)
+constexpr uint32_t kDMChunksMax = 1024;  // chunks per block (int32 product tiles: 2 MFMAs, 2^20 per chunk)
+static_assert(2ull * (1u << 19) * kDMChunksMax <= (1ull << 30), "dm tile bound");
 struct DMScratch {
   uint8_t img[kDCats][4][kDMQuads][32];  // 64 KB: category, table, quad, digit row
   uint8_t wimg[3][32][32];                // digit rows of the fold constants (c, k)
@@ -571,7 +573,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, 
 // ---------------------------------------------------------------------------
 constexpr int kD0TCats = 27;
 constexpr int kD0TLimbs = kD0TCats * 9;  // 243 limb sums (9 words per category, congruent mod p)
-constexpr uint32_t kD0TChunksMax = 512;  // chunks per block: a tile slot takes <= 8 MFMAs (2^22) per chunk
+// chunks per block: the busiest tile slot of a wave takes 4 of its 16 MFMAs
+// per chunk (4 x 2^19 = 2^21), so 512 chunks keep |slot| <= 2^30
+constexpr uint32_t kD0TChunksMax = 512;
+static_assert(4ull * (1u << 19) * kD0TChunksMax <= (1ull << 30), "d0t tile bound");
 // moment digit of one axis: corners (x, y) -> 0, 1 or 2 (= s)
 __host__ __device__ constexpr int moment_digit(int x, int y) { return x == y ? x : 2; }
 
@@ -856,8 +861,18 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm3(const Fe* __restrict__ A,
 // pattern than 32 octants x two corners, and 476 vs 499 us for the first
 // triple step) and a single-buffered image — for large levels; 32 octants, two
 // corners per fold and a double-buffered image — twice the blocks for small ones.
+// int32 tile bound: an MFMA adds at most 32 x 128^2 = 2^19 in magnitude to a
+// slot, and the busiest slot (moment s on both b and c: 4 of a wave's 16
+// corner-pair products) takes 4 MFMAs per (product, K half): 16 per chunk of
+// 64 octants, 8 per chunk of 32. A block's chunk count stays <= kT33ChunksMax
+// (the host sizes the grid so, step_grid), so |slot| <= 2^30 (the
+// previous 256 / 512 reached exactly 2^31).
 template <int OCT>
-constexpr uint32_t kT33ChunksMax = OCT == 64 ? 256 : 512;  // a tile slot takes <= 16 (8) MFMAs per chunk
+constexpr uint32_t kT33SlotMfmas = OCT == 64 ? 16 : 8;
+template <int OCT>
+constexpr uint32_t kT33ChunksMax = OCT == 64 ? 128 : 256;
+static_assert((uint64_t)kT33SlotMfmas<64> * (1u << 19) * kT33ChunksMax<64> <= (1ull << 30), "t33 tile bound");
+static_assert((uint64_t)kT33SlotMfmas<32> * (1u << 19) * kT33ChunksMax<32> <= (1ull << 30), "t33 tile bound");
 struct T33Scratch {
   uint8_t img[2][8][4][32][32];  // [buffer][corner][table][octant][digit row] (OCT 32), or [corner][table][64][32] (OCT 64)
   unsigned long long T[kD0TCats][64];

@@ -54,6 +54,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_D0")) c->d0 = atoi(e);
     if (const char* e = getenv("ZK_CIRCUIT_DENSE")) c->circuit_dense = atoi(e) != 0;
     if (const char* e = getenv("ZK_DTAIL_MAX_QUADS")) c->dtail_max_quads = strtoull(e, nullptr, 0);
+    if (const char* e = getenv("ZK_GRID_CAP")) c->grid_cap = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_ATOMIC_FANIN")) c->atomic_fanin = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_DTAIL_BLOCKS")) c->dtail_blocks = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_GATHER_VARS")) c->gather_vars = (uint32_t)strtoul(e, nullptr, 0);
