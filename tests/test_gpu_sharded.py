@@ -59,27 +59,6 @@ def _oracle(field: int, n: int) -> dict:
             "blob_keccak": po.keccak256(po.proof_blob(po.BLOB_GKR, field, 0, [list(p) for p in polys])).hex()}
 
 
-def _steps(nloc: int, d0: bool = True) -> int:
-    """Kernel steps of a phase of nloc rounds, one all-reduce each: round 0,
-    round 1, one more single round if nloc - 2 is odd, then two rounds per step.
-    With ZK_D0 (default) an even phase runs rounds 0 and 1 in one step; a phase
-    of >= 11 rounds (ZK_D0T) rounds 0-2, nt triple steps, one two-round step
-    folding by three, then two rounds per step."""
-    if d0 and nloc >= 11:  # three rounds per pass (host.hpp gkr_phase): d0t, nt triples, one fold-by-three double, doubles
-        nt, k = -1, 0
-        while 3 + 3 * k + 8 <= nloc:
-            r = nloc - 3 - 3 * k
-            if r % 2 == 0 and (r >= 12 or nt < 0):
-                nt = k
-            k += 1
-        return 1 + nt + 1 + (nloc - 5 - 3 * nt) // 2
-    if d0 and nloc >= 2 and nloc % 2 == 0:
-        return nloc // 2
-    if nloc <= 2:
-        return nloc
-    return 2 + (nloc - 2) % 2 + (nloc - 2) // 2
-
-
 def _bounds(nloc: int, d0: bool = True) -> list[int]:
     """End round of each step of a sharded phase (no persistent steps across
     ranks), as host.hpp gkr_phase builds the schedule."""
@@ -148,11 +127,17 @@ def test_world1_without_comm(tmp_path):
     assert res[0]["collectives"] == 0
 
 
-def test_rccl_data_path_forced_at_world1(tmp_path):
-    res = _run(1, "rccl", 0, 14, str(tmp_path), {"ZK_FORCE_COLLECTIVES": "1"})
-    want = _oracle(0, 14)
+@pytest.mark.parametrize("nloc,gather", [(14, "0"), (14, "10"), (20, "10"), (13, "6")])
+def test_rccl_data_path_forced_at_world1(tmp_path, nloc, gather):
+    """ZK_FORCE_COLLECTIVES=1 runs a world-1 proof through the sharded code
+    path over RCCL: every step's sums through ncclAllReduce + the publish
+    kernel until the gather boundary, then the early gather as an in-place
+    ncclAllGather (host.hpp gkr_prove_device) and k_interleave (gather 0:
+    every step, then the one-element-per-table gather through the all-reduce)."""
+    res = _run(1, "rccl", 0, nloc, str(tmp_path), {"ZK_FORCE_COLLECTIVES": "1", "ZK_GATHER_VARS": gather})
+    want = _oracle(0, nloc)
     assert {"polys": res[0]["polys"], "chal": res[0]["chal"], "blob_keccak": res[0]["blob_keccak"]} == want
-    assert res[0]["collectives"] == _steps(14)  # every step went through ncclAllReduce
+    assert res[0]["collectives"] == _collectives(nloc, int(gather))
 
 
 @pytest.mark.parametrize("comm,world,nloc", [("host", 2, 10), ("rccl", 1, 12)])
@@ -166,7 +151,7 @@ def test_first_double_step_sharded(tmp_path, comm, world, nloc):
     want = _oracle(0, nloc + world.bit_length() - 1)
     for rank, r in enumerate(res):
         assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
-        assert r["collectives"] == (_collectives(nloc) if world > 1 else _steps(nloc, d0=True))
+        assert r["collectives"] == _collectives(nloc)
 
 
 @pytest.mark.parametrize("world,nloc,field,gather", [(2, 16, 0, "0"), (2, 16, 2, "4"), (4, 13, 1, "6"), (2, 20, 0, "10"),
@@ -179,6 +164,20 @@ def test_early_gather_matches_single_process(tmp_path, world, nloc, field, gathe
     Every setting gives every rank the single-process oracle's proof."""
     res = _run(world, "host", field, nloc, str(tmp_path), {"ZK_GATHER_VARS": gather})
     want = _oracle(field, nloc + world.bit_length() - 1)
+    for rank, r in enumerate(res):
+        assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
+        assert r["collectives"] == _collectives(nloc, int(gather)), f"rank {rank}"
+
+
+# G = 8, the world size of the 8-GPU node, on this one card: 8 worker
+# processes (host all-reduce over gloo; RCCL refuses ranks that share a
+# device). Exercises the 8-way low-bit shard layout, the [8][4][2^T] gather
+# buffer, the 8-way k_interleave and the last log2(8) = 3 rounds that every
+# rank finishes locally (gather 0: the one-element-per-table gather).
+@pytest.mark.parametrize("nloc,field,gather", [(10, 0, "10"), (14, 0, "0"), (13, 2, "10"), (12, 1, "6"), (14, 0, "10")])
+def test_world8_host_comm_matches_single_process(tmp_path, nloc, field, gather):
+    res = _run(8, "host", field, nloc, str(tmp_path), {"ZK_GATHER_VARS": gather})
+    want = _oracle(field, nloc + 3)
     for rank, r in enumerate(res):
         assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
         assert r["collectives"] == _collectives(nloc, int(gather)), f"rank {rank}"

@@ -204,6 +204,7 @@ struct zk_ctx {
   zk_allreduce_u64_fn ar = nullptr;
   bool force_coll = false;  // debug: run the collective path even at world 1 (ZK_FORCE_COLLECTIVES)
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
+  bool host_prelaunch = false;  // ... also under a host communicator (ZK_HOST_PRELAUNCH; ranks on distinct devices only)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
   int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
   bool d0t = true;          // nv >= 11: rounds 0-2 in one pass, then steps that fold by three (ZK_D0T)
@@ -324,6 +325,7 @@ void launch(zk_ctx* c, int kind, double bytes, double muls, Kern kernel, uint32_
   c->stats.alg_bytes[kind] += bytes;
   c->stats.field_muls[kind] += muls;
 }
+constexpr size_t kLaunchLogMax = 1 << 16;  // launch_log entries kept (bounded)
 // after a stream sync: fold event timings into the stats
 inline void flush_timing(zk_ctx* c) {
   static const bool dbg = getenv("ZK_DEBUG_EVENTS") != nullptr;
@@ -332,6 +334,8 @@ inline void flush_timing(zk_ctx* c) {
     HIPCK(hipEventElapsedTime(&ms, p.a, p.b));
     if (dbg) fprintf(stderr, "zk: kind %d %.1f us\n", p.kind, ms * 1e3);
     c->stats.kernel_ms[p.kind] += ms;
+    if (c->launch_log.size() >= kLaunchLogMax)  // a context timed for a long time keeps the newest launches
+      c->launch_log.erase(c->launch_log.begin(), c->launch_log.begin() + kLaunchLogMax / 2);
     c->launch_log.push_back(zk_launch{p.kind, (double)ms, p.bytes});
     c->ev_free.push_back({p.a, p.b});
   }
@@ -525,7 +529,12 @@ struct PostR {
 // ranks that share one device would starve each other — a pre-enqueued step
 // spinning on its challenge holds the CUs the other rank's producing kernel
 // needs. Each step then launches after its challenge (same proof).
-inline bool prelaunch(zk_ctx* c, uint32_t nv) { return c->prelaunch && nv > 1 && c->comm != COMM_HOST; }
+// ZK_HOST_PRELAUNCH=1 keeps pre-enqueue under a host communicator: for callers
+// whose ranks each own a device and whose callback answers well inside the
+// kernels' 1 s challenge guard (the library cannot see either from here).
+inline bool prelaunch(zk_ctx* c, uint32_t nv) {
+  return c->prelaunch && nv > 1 && (c->comm != COMM_HOST || c->host_prelaunch);
+}
 
 // Run `nv` rounds over 4 device tables of 2^nv elements starting at global
 // round k0, as a sequence of steps:
@@ -1337,18 +1346,24 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
   uint32_t pend = 0;
   uint32_t stop = nloc;
-  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend, lg == 0,  // one rank: the final tables are not needed
-               lg > 0 ? c->gather_vars : 0, &stop);
-  if (lg == 0) {
+  // the collective path: more than one rank, or (ZK_FORCE_COLLECTIVES with a
+  // communicator) one rank through the same code, early gather included
+  const bool coll = sharded && (lg > 0 || (c->force_coll && c->comm != COMM_NONE));
+  gkr_phase<F>(c, cur, nloc, 0, sharded, tr, out, claim, r, pend, !coll,  // one rank: the final tables are not needed
+               coll ? c->gather_vars : 0, &stop);
+  if (!coll) {
     sync(c);  // settles event timings; the results are already on the host
     return;
   }
   if (stop < nloc) {
     // ---- early gather: T = nloc - stop local rounds remain. Every rank folds
     // its tables by the pending challenges (r_{stop-pend} .. r_{stop-1}) to 4 x
-    // 2^T, writes them into its slot of a zeroed one-hot buffer [G][4][2^T]
-    // (exact under a u64 SUM: every word has one nonzero contributor), one
-    // all-reduce gathers every rank's slot, k_interleave lays out the global
+    // 2^T into its slot of a buffer [G][4][2^T]; ONE collective gathers every
+    // rank's slot (RCCL: an in-place ncclAllGather, 4 x 2^T x 32 B sent per
+    // rank, 128 KiB at T = 10; a host communicator only offers a SUM
+    // all-reduce, so there the buffer is zeroed first and the all-reduce is
+    // exact because every word has one nonzero contributor — G times the
+    // bytes, a test / diagnostic path), k_interleave lays out the global
     // tables (index m G + g), and every rank runs the last T + lg rounds
     // locally, with no further collective: the small steps, whose latency an
     // all-reduce per step would dominate, run in the persistent tail and on
@@ -1361,7 +1376,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
     Fe* sc = reinterpret_cast<Fe*>(c->gbuf.p);
     Fe* oh = sc + scratch;
     Fe* gl = oh + onehot;
-    HIPCK(hipMemsetAsync(oh, 0, onehot * sizeof(Fe), c->stream));
+    if (c->comm != COMM_RCCL) HIPCK(hipMemsetAsync(oh, 0, onehot * sizeof(Fe), c->stream));
     Fe* slot = oh + (size_t)c->rank * 4 * Tn;
     if (pend == 0) {
       for (int t = 0; t < 4; ++t) HIPCK(hipMemcpyAsync(slot + t * Tn, cur[t], Tn * 32, hipMemcpyDeviceToDevice, c->stream));
@@ -1375,8 +1390,8 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
              cur[2], cur[3], dst, dst + dstride, dst + 2 * dstride, dst + 3 * dstride, half, rj);
       for (int t = 0; t < 4; ++t) cur[t] = dst + t * dstride;
     }
-    if (c->comm == COMM_RCCL) {
-      NCCLCK(ncclAllReduce(oh, oh, onehot * 4, ncclUint64, ncclSum, c->nccl, c->stream));
+    if (c->comm == COMM_RCCL) {  // in place: this rank's slot is its send buffer
+      NCCLCK(ncclAllGather(slot, oh, (size_t)4 * Tn * 4, ncclUint64, c->nccl, c->stream));
       c->stats.collectives += 1;
     } else {
       std::vector<uint64_t> w(onehot * 4);

@@ -44,6 +44,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_LANES_MAX_PAIRS")) c->lanes_max_pairs = strtoull(e, nullptr, 0);  // tuning knob
     if (const char* e = getenv("ZK_FORCE_COLLECTIVES")) c->force_coll = atoi(e) != 0;
     if (const char* e = getenv("ZK_PRELAUNCH")) c->prelaunch = atoi(e) != 0;
+    if (const char* e = getenv("ZK_HOST_PRELAUNCH")) c->host_prelaunch = atoi(e) != 0;
     if (const char* e = getenv("ZK_TAIL")) c->tail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DROUND")) c->dround = atoi(e) != 0;
     if (const char* e = getenv("ZK_DTAIL")) c->dtail = atoi(e) != 0;
