@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 11u
+#define ZK_ABI_VERSION 12u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -118,6 +118,16 @@ void zk_transcript_free(zk_transcript* t);
 int zk_transcript_append(zk_transcript* t, const uint8_t* data, size_t len); /* append :19-21 */
 int zk_transcript_get_random_challenge(zk_transcript* t, zk_field field, zk_repr repr,
                                        zk_fe* out);          /* get_random_challenge   :23-29 */
+/* Checkpoint / resume of a transcript mid-proof. The reference's
+ * Transcript derives Clone (:5) but not serde; this is the byte image of that clone:
+ *   "ZKTR" | u32 version (1) | u32 fill (< 136) | u32 0 | 25 x u64 LE Keccak lanes |
+ *   136 bytes of the partial rate block (bytes >= fill are zero)
+ * = ZK_TRANSCRIPT_STATE_BYTES. A deserialised transcript continues bit-exactly where the
+ * serialised one stood (same challenges for the same appends). zk_transcript_deserialize
+ * returns NULL on a bad magic / version / fill / non-zero padding or len != the size. */
+#define ZK_TRANSCRIPT_STATE_BYTES 352
+int zk_transcript_serialize(const zk_transcript* t, uint8_t* out, size_t cap, size_t* out_len);
+zk_transcript* zk_transcript_deserialize(const uint8_t* data, size_t len);
 /* fq_vec_to_bytes :32-37 — canonical LE, 32 bytes per element into out[32*n] */
 int zk_fe_vec_to_bytes(zk_field field, zk_repr repr, const zk_fe* v, size_t n, uint8_t* out);
 

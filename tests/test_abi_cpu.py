@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().zk_abi_version() == _lib.ABI_VERSION == 11
+    assert _lib.lib().zk_abi_version() == _lib.ABI_VERSION == 12
 
 
 def test_nm_exports_match_header():
@@ -175,3 +175,36 @@ def test_kernel_kinds_match_header():
     assert total == len(_lib.KERNEL_KINDS)
     alias = {"gkr_lanes": "gkr_round_lanes"}  # header name -> mirror name
     assert [alias.get(k, k) for k in sorted(kinds, key=kinds.get)] == _lib.KERNEL_KINDS
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
+def test_transcript_serialize_roundtrip(field):
+    """Checkpoint / resume: a transcript restored from its bytes continues
+    exactly like the original and like the oracle, at every fill of the rate block."""
+    o = po.Transcript(field)
+    t = zk_amd.Transcript(field)
+    for chunk in [b"", b"a", bytes(range(135)), b"\x07" * 136, b"y" * 137, bytes(300)]:
+        t.append(chunk)
+        o.append(chunk)
+        state = t.to_bytes()
+        assert len(state) == 352 and state[:4] == b"ZKTR"
+        r = zk_amd.Transcript.from_bytes(state, field)
+        assert r.to_bytes() == state
+        want = o.get_random_challenge()
+        assert r.get_random_challenge() == want
+        assert t.get_random_challenge() == want
+        assert r.to_bytes() == t.to_bytes()
+
+
+def test_transcript_deserialize_rejects_malformed():
+    t = zk_amd.Transcript(0)
+    t.append(b"abc")
+    s = bytearray(t.to_bytes())
+    assert zk_amd.Transcript.from_bytes(bytes(s)).get_random_challenge() == t.clone().get_random_challenge()
+    bad = [bytes(s[:-1]), bytes(s) + b"\0", b"XKTR" + bytes(s[4:]),
+           bytes(s[:4]) + (2).to_bytes(4, "little") + bytes(s[8:]),
+           bytes(s[:8]) + (136).to_bytes(4, "little") + bytes(s[12:]),
+           bytes(s[:-1]) + b"\x01", b""]
+    for b in bad:
+        with pytest.raises(ValueError):
+            zk_amd.Transcript.from_bytes(b)

@@ -161,6 +161,32 @@ int zk_transcript_append(zk_transcript* t, const uint8_t* data, size_t len) {
     t->h.update(data, len);
   });
 }
+int zk_transcript_serialize(const zk_transcript* t, uint8_t* out, size_t cap, size_t* out_len) {
+  return guarded([&] {
+    require(t && out_len, "null argument");
+    *out_len = ZK_TRANSCRIPT_STATE_BYTES;
+    require(out && cap >= ZK_TRANSCRIPT_STATE_BYTES, "output buffer smaller than ZK_TRANSCRIPT_STATE_BYTES");
+    const uint32_t head[4] = {0x52544b5au /* "ZKTR" */, 1u, (uint32_t)t->h.fill, 0u};
+    memcpy(out, head, 16);
+    memcpy(out + 16, t->h.st, 200);  // little-endian host: lanes as u64 LE
+    memset(out + 216, 0, zk::Keccak256::RATE);
+    memcpy(out + 216, t->h.buf, t->h.fill);
+  });
+}
+zk_transcript* zk_transcript_deserialize(const uint8_t* data, size_t len) {
+  if (!data || len != ZK_TRANSCRIPT_STATE_BYTES) return nullptr;
+  uint32_t head[4];
+  memcpy(head, data, 16);
+  if (head[0] != 0x52544b5au || head[1] != 1u || head[2] >= zk::Keccak256::RATE || head[3] != 0) return nullptr;
+  for (size_t i = 216 + head[2]; i < ZK_TRANSCRIPT_STATE_BYTES; ++i)
+    if (data[i]) return nullptr;
+  zk_transcript* t = new (std::nothrow) zk_transcript();
+  if (!t) return nullptr;
+  memcpy(t->h.st, data + 16, 200);
+  memcpy(t->h.buf, data + 216, head[2]);
+  t->h.fill = head[2];
+  return t;
+}
 int zk_transcript_get_random_challenge(zk_transcript* t, zk_field field, zk_repr repr, zk_fe* out) {
   return guarded([&] {
     require(t && out, "null argument");

@@ -17,7 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-ABI_VERSION = 11  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
+ABI_VERSION = 12  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
 KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33"]
 
 
@@ -63,6 +63,8 @@ SIGNATURES = {
     "zk_transcript_free": (None, [P]),
     "zk_transcript_append": (I, [P, P, SZ]),
     "zk_transcript_get_random_challenge": (I, [P, I, I, P]),
+    "zk_transcript_serialize": (I, [P, P, SZ, C.POINTER(SZ)]),
+    "zk_transcript_deserialize": (P, [P, SZ]),
     "zk_fe_vec_to_bytes": (I, [I, I, P, SZ, P]),
     "zk_mle_partial_evaluate": (I, [P, I, I, P, U32, U32, P, P]),
     "zk_mle_evaluate": (I, [P, I, I, P, U32, P, U32, P]),

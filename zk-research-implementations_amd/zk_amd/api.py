@@ -98,6 +98,23 @@ class Transcript:
     def clone(self) -> "Transcript":
         return Transcript(self.field, _handle=lib().zk_transcript_clone(self.h))
 
+    def to_bytes(self) -> bytes:
+        """Checkpoint: the byte image of `clone()` (zk_transcript_serialize)."""
+        out = (C.c_uint8 * 352)()
+        n = C.c_size_t(0)
+        _call(lib().zk_transcript_serialize(self.h, out, len(out), C.byref(n)))
+        return bytes(out[: n.value])
+
+    @classmethod
+    def from_bytes(cls, state: bytes, field: int = Field.BN254_FR) -> "Transcript":
+        """Resume from `to_bytes()`; ValueError on a malformed state."""
+        b = bytes(state)
+        buf = (C.c_uint8 * max(1, len(b))).from_buffer_copy(b or b"\0")
+        h = lib().zk_transcript_deserialize(buf, len(b))
+        if not h:
+            raise ValueError("malformed transcript state")
+        return cls(field, _handle=h)
+
 
 def fq_vec_to_bytes(values, field: int = Field.BN254_FR) -> bytes:
     a = as_limbs(values)
