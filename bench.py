@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--nvars", type=int, default=24, help="variables per GPU")
     ap.add_argument("--field", default="bn254_fr", choices=sorted(FIELDS))
     ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--cpu-sample-nvars", type=int, default=22)
+    ap.add_argument("--cpu-sample-nvars", type=int, default=24,
+                    help="size of the single-thread reference-faithful CPU run (24 = the headline workload)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-tables (PCIe-inclusive) prove")
@@ -53,6 +54,8 @@ def parse():
     ap.add_argument("--force-rccl", action="store_true",
                     help="diagnostic: at world 1 route every step through ncclAllReduce (the multi-rank data path)")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
+    ap.add_argument("--no-plain", action="store_true",
+                    help="skip BASELINE config 1 (12-var plain prove, CPU port) and the GPU plain prove/verify legs")
     return ap.parse_args()
 
 
@@ -96,6 +99,106 @@ def cpu_model() -> str:
     return platform.processor()
 
 
+def _ranges(cpus) -> str:
+    """[0,1,2,5] -> '0-2,5'"""
+    out, start, prev = [], None, None
+    for c in cpus:
+        if start is None:
+            start = prev = c
+        elif c == prev + 1:
+            prev = c
+        else:
+            out.append(f"{start}-{prev}" if prev > start else f"{start}")
+            start = prev = c
+    if start is not None:
+        out.append(f"{start}-{prev}" if prev > start else f"{start}")
+    return ",".join(out)
+
+
+def config1_bench(ctx, field: int, nvars: int = 12, runs: int = 101) -> dict:
+    """BASELINE config 1: the reference's own benchmark shape
+    (sum_check/benches/sum_check_benchmark.rs:9-31 — criterion over `prove` of a
+    12-var random BN254 Fr MultilinearPoly): the reference-faithful C port
+    (oracle/zk_oracle.c or_sumcheck_prove, one thread) as the median of `runs`
+    proves after 10 warm-up, and the GPU library's `prove` on the same table."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle as co  # baseline/checker only
+
+    import zk_amd
+
+    evals = co.synth(field, 1, 0, 0, 1 << nvars)
+    cpu = []
+    for i in range(runs + 10):
+        t0 = time.perf_counter()
+        rp, cs = co.prove(field, evals)
+        if i >= 10:
+            cpu.append(time.perf_counter() - t0)
+    poly = zk_amd.MultilinearPoly(evals, field, ctx)
+    gpu = []
+    for i in range(runs + 10):
+        t0 = time.perf_counter()
+        proof = zk_amd.prove(poly, ctx=ctx)
+        if i >= 10:
+            gpu.append(time.perf_counter() - t0)
+    same = [v for p in proof.proof_polynomials for v in p] == co.from_limbs(rp.reshape(-1, 4)) \
+        and proof.claimed_sum == cs
+    cpu.sort()
+    gpu.sort()
+    ops = 6.0 * ((1 << nvars) - 1)
+    return {
+        "workload": f"sum_check prove, {nvars}-var BN254 Fr MultilinearPoly (seed 1), shape of "
+        "sum_check_benchmark.rs:9-31",
+        "cpu_port_median_us": cpu[len(cpu) // 2] * 1e6,
+        "cpu_port_field_ops_per_s": ops / cpu[len(cpu) // 2],
+        "cpu_cores": 1,
+        "gpu_median_us": gpu[len(gpu) // 2] * 1e6,
+        "runs": runs,
+        "same_proof": bool(same),
+        "note": "at 12 variables the GPU call is launch- and hand-off-bound (12 rounds, host transcript "
+        "absorbs the 128 KiB table first); the GPU leg is for completeness, the CPU port is the config-1 number",
+    }
+
+
+def plain_bench(ctx, field: int, nvars: int, reps: int = 2) -> dict:
+    """GPU plain `prove` / `verify` (sum_check_protocol.rs:25-84) at scale, from host
+    tables (the ABI takes host evaluations), with the serial host Keccak absorb of
+    the 32 N table bytes that the protocol starts with (:27, F6) timed on its own:
+    it is the Amdahl floor of plain `prove` on any device."""
+    import ctypes as C
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+
+    evals = ctx.synth(field, 1 << nvars, seed=1, table=0).download()  # canonical host limbs
+    poly = zk_amd.MultilinearPoly(evals, field, ctx)
+    out = (C.c_uint8 * 32)()
+    ka = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        check(lib().zk_keccak256(evals.ctypes.data, evals.nbytes, out))
+        ka.append(time.perf_counter() - t0)
+    pv, vf = [], []
+    ok = True
+    for i in range(reps + 1):
+        t0 = time.perf_counter()
+        proof = zk_amd.prove(poly, ctx=ctx)
+        t1 = time.perf_counter()
+        ok = ok and zk_amd.verify(poly, proof, ctx=ctx)
+        t2 = time.perf_counter()
+        if i:
+            pv.append(t1 - t0)
+            vf.append(t2 - t1)
+    med = lambda v: sorted(v)[len(v) // 2] * 1e3  # noqa: E731
+    return {
+        "workload": f"plain prove + verify, {nvars}-var BN254 Fr table from host memory ({evals.nbytes / 2**20:.0f} MiB)",
+        "prove_ms": med(pv),
+        "verify_ms": med(vf),
+        "host_keccak_absorb_ms": med(ka),
+        "absorb_share_of_prove": med(ka) / med(pv),
+        "verified": bool(ok),
+    }
+
+
 def cpu_baseline(field: int, nvars: int, fast_nvars: int) -> dict:
     """Reference CPU path: the C restatement of the reference prover
     (oracle/zk_oracle.c, same algorithm and allocation pattern as
@@ -118,11 +221,18 @@ def cpu_baseline(field: int, nvars: int, fast_nvars: int) -> dict:
     co.gkr_prove(field, ftabs, co.Transcript(), fast=True)
     dtf = time.perf_counter() - t0
     del ftabs
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = list(range(os.cpu_count() or 1))
     return {
         "value": ops / dt,
         "unit": "field-ops/s",
         "cores": 1,
         "kind": "port",
+        "nproc": os.cpu_count(),
+        "affinity_cpus": len(aff),
+        "affinity_mask": _ranges(aff),
         "sample": f"one gkr_prove over a {nvars}-var synthetic SumPoly (4 tables x 2^{nvars}), "
         f"{dt:.2f} s single-thread, host '{cpu_model()}' ({os.cpu_count()} logical CPUs)",
         "prover_ms_sample": dt * 1e3,
@@ -131,6 +241,9 @@ def cpu_baseline(field: int, nvars: int, fast_nvars: int) -> dict:
             "unit": "field-ops/s",
             "cores": co.threads(),
             "kind": "port (fused OpenMP restatement, oracle/zk_oracle.c or_gkr_prove_fast)",
+            "threads_note": "OpenMP threads = OMP_NUM_THREADS (the GPU box's CPU share per GPU is 16 of its "
+            f"{os.cpu_count()} logical CPUs; affinity mask {_ranges(aff)}), so this is every thread the lease allows",
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"one gkr_prove over {nf} vars (4 tables x 2^{nf}, same seed as the GPU run)",
             "prover_ms": dtf * 1e3,
         },
@@ -588,6 +701,9 @@ def main() -> None:
             out["gkr_circuit"] = circuit_bench(ctx, field)
         if not args.no_config5 and world == 1:
             out["config5_bls12_381"] = config5_bench(ctx)
+        if not args.no_plain and world == 1:
+            out["config1_12var_prove"] = config1_bench(ctx, field)
+            out["plain_sumcheck"] = [plain_bench(ctx, field, nv) for nv in (20, 24)]
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(field, args.cpu_sample_nvars, args.cpu_fast_nvars)
             out["cpu_baseline"] = cb

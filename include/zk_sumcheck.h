@@ -268,6 +268,26 @@ int zk_g2_mul_generator(zk_repr repr, const zk_fe* scalars, size_t n, zk_g2* out
 int zk_bls12_381_pairing(const zk_g1* p, const zk_g2* q, uint64_t out[72]);
 int zk_bls12_381_pairing_check(const zk_g1* p, const zk_g2* q, size_t n, int* out_ok);
 
+/* gkr::prove WITH the input layer's KZG step (gkr_protocol.rs:92-118), so the
+ * proof is the reference's GkrProof including input_proof. BLS12-381 Fr only
+ * (the reference's KZG is over BLS12-381, kzg.rs:3). The reference draws the
+ * taus from StdRng::from_entropy (:97-103); here they are the caller's
+ * taus[log2 ninputs] so proofs are reproducible. Writes everything
+ * zk_gkr_circuit_prove writes (out_input_evals = the two values KZG::open
+ * returns at r_b and r_c), plus the commitment (KZG::commit :106), the two
+ * get_proof results out_proofs[2 log2 ninputs] (w_b's then w_c's, :108-113)
+ * and the verifier's setup out_g2_taus[log2 ninputs] (KZG::g2_taus). */
+int zk_gkr_circuit_prove_kzg(zk_ctx* ctx, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                             const zk_fe* inputs, uint32_t ninputs, const zk_fe* taus, zk_fe* out_output_poly,
+                             zk_fe* out_coeffs, uint8_t* out_ncoeffs, zk_fe* out_challenges, zk_fe* out_claims,
+                             zk_fe* out_input_evals, zk_g1* out_commitment, zk_g1* out_proofs, zk_g2* out_g2_taus);
+/* gkr::verify (:128-227) with the two KZG::verify checks of the input layer
+ * (:155-175) at the verifier's own (r_b, r_c): needs no inputs. */
+int zk_gkr_circuit_verify_kzg(zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                              const zk_fe* output_poly, const zk_fe* coeffs, const uint8_t* ncoeffs,
+                              const zk_fe* claims, const zk_fe* opened_evals, const zk_g1* commitment,
+                              const zk_g1* proofs, const zk_g2* g2_taus, int* out_verified);
+
 /* ---------------------------------------------------------------------------
  * Proof blob: a canonical byte form of a proof, so a proof
  * produced on the CPU, on one GPU or on G GPUs can be compared as one digest

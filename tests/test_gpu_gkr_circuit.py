@@ -91,3 +91,43 @@ def test_large_circuit_verifies(ctx, field):
     bad = list(inputs)
     bad[123] = (bad[123] + 1) % p
     assert not verify(proof, circ, bad)
+
+
+@pytest.mark.parametrize("taus", [[5, 2, 3], [0x1234567, 99, 0xdeadbeefcafef00d]])
+def test_reference_circuit_with_input_kzg(ctx, taus):
+    """gkr::prove including the input layer's KZG step (gkr_protocol.rs:92-118)
+    with caller-fixed taus, on the reference's 8-input circuit (:473-506): every
+    field of the proof equals gkr_oracle + kzg_oracle (commit and both
+    get_proofs against the Lagrange basis of the taus), and gkr::verify's KZG
+    checks (:155-175, two pairings per opening on the host) accept it and
+    reject tampered openings, commitments and proofs."""
+    import dataclasses
+
+    import kzg_oracle as ko
+    import pairing_oracle as pa
+
+    structure = [[A, A, A, A], [M, A], [A]]
+    inputs = [5, 2, 2, 4, 10, 0, 3, 3]
+    circ = Circuit([[OPS[o] for o in layer] for layer in structure], 2)
+    got = prove(circ, inputs, ctx, taus=taus)
+    want = go.prove(2, structure, inputs)
+    assert [[q.coefficient for q in layer] for layer in got.proof_polynomials] == \
+        [[list(q) for q in layer] for layer in want["proof_polynomials"]]
+    assert got.claimed_evaluations == [tuple(c) for c in want["claimed_evaluations"]]
+    kp = got.input_proof
+    basis = ko.get_lagrange_basis(taus)
+    assert kp.commitment == ko.commit(inputs, basis)
+    assert kp.opened_evals == tuple(want["input_evaluations"])
+    assert kp.opened_evals == (ko.open_(inputs, want["final_rb"]), ko.open_(inputs, want["final_rc"]))
+    assert list(kp.proof[0]) == ko.get_proof(inputs, kp.opened_evals[0], want["final_rb"], basis)
+    assert list(kp.proof[1]) == ko.get_proof(inputs, kp.opened_evals[1], want["final_rc"], basis)
+    assert kp.g2_taus == pa.g2_taus(taus)
+    assert verify(got, circ)  # no inputs: the verifier trusts only the commitment
+    bad_open = dataclasses.replace(kp, opened_evals=(kp.opened_evals[0] + 1, kp.opened_evals[1]))
+    assert not verify(dataclasses.replace(got, input_proof=bad_open), circ)
+    bad_com = dataclasses.replace(kp, commitment=ko.add(kp.commitment, ko.G1))
+    assert not verify(dataclasses.replace(got, input_proof=bad_com), circ)
+    bad_prf = dataclasses.replace(kp, proof=(kp.proof[1], kp.proof[0]))
+    assert not verify(dataclasses.replace(got, input_proof=bad_prf), circ)
+    with pytest.raises(ValueError):
+        prove(Circuit([[OPS[o] for o in layer] for layer in structure], 0), inputs, ctx, taus=taus)

@@ -258,7 +258,8 @@ Fe mle_eval_host(std::vector<Fe> t, const std::vector<Fe>& pt) {  // Multilinear
 template <class F>
 bool gkr_circuit_verify_host(zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
                              const zk_fe* inputs, uint32_t ninputs, const zk_fe* output_poly, const zk_fe* coeffs,
-                             const uint8_t* ncoeffs, const zk_fe* claims, const zk_fe* input_evals) {
+                             const uint8_t* ncoeffs, const zk_fe* claims, const zk_fe* input_evals,
+                             std::vector<Fe>* last_chal = nullptr) {
   using namespace zk;
   std::vector<size_t> opoff(nlayers + 1, 0);
   for (uint32_t l = 0; l < nlayers; ++l) opoff[l + 1] = opoff[l] + gates[l];
@@ -301,6 +302,7 @@ bool gkr_circuit_verify_host(zk_repr repr, uint32_t nlayers, const uint32_t* gat
     }
     k0 += nv;
     Fe o1, o2;
+    if (idx + 1 == nlayers && last_chal) *last_chal = chal;
     if (idx + 1 == nlayers) {
       o1 = in_mont<F>(repr, input_evals[0]);
       o2 = in_mont<F>(repr, input_evals[1]);
@@ -391,6 +393,72 @@ int zk_gkr_circuit_verify(zk_field field, zk_repr repr, uint32_t nlayers, const 
                           : 0;
     });
   });
+}
+
+// ---- gkr::prove / gkr::verify with the input layer's KZG step (gkr_protocol.rs:92-118, :155-175) ----
+// A composition of the entry points above: the circuit proof (GPU), then
+// KZG::new over the caller's taus (GPU setup), commit (GPU MSM), the two
+// openings KZG::open returns (= the input evaluations the circuit prover
+// computed at r_b, r_c) and their get_proofs (GPU), and the G2 taus.
+int zk_gkr_circuit_prove_kzg(zk_ctx* c, zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                             const zk_fe* inputs, uint32_t ninputs, const zk_fe* taus, zk_fe* out_output_poly,
+                             zk_fe* out_coeffs, uint8_t* out_ncoeffs, zk_fe* out_challenges, zk_fe* out_claims,
+                             zk_fe* out_input_evals, zk_g1* out_commitment, zk_g1* out_proofs, zk_g2* out_g2_taus) {
+  int rc = guarded([&] {
+    require(c && inputs && taus && out_commitment && out_proofs && out_g2_taus && out_challenges, "null argument");
+    check_circuit(nlayers, gates, ops, ninputs);
+  });
+  if (rc != ZK_OK) return rc;
+  rc = zk_gkr_circuit_prove(c, ZK_BLS12_381_FR, repr, nlayers, gates, ops, inputs, ninputs, out_output_poly,
+                            out_coeffs, out_ncoeffs, out_challenges, out_claims, out_input_evals);
+  if (rc != ZK_OK) return rc;
+  const uint32_t nin = lg2u(ninputs);
+  const uint32_t total = circuit_rounds(nlayers, gates);
+  const zk_fe* rb = out_challenges + (total - 2 * nin);  // the input layer's sum-check: (r_b, r_c) (:71-73)
+  const zk_fe* rcp = rb + nin;
+  zk_kzg* k = nullptr;
+  rc = zk_kzg_setup(c, repr, taus, nin, &k);  // KZG::new(&input_poly, taus) (:105)
+  if (rc == ZK_OK) rc = zk_kzg_commit(c, k, repr, inputs, out_commitment);  // :106
+  if (rc == ZK_OK) rc = zk_kzg_get_proof(c, k, repr, inputs, &out_input_evals[0], rb, out_proofs);  // :108-110
+  if (rc == ZK_OK) rc = zk_kzg_get_proof(c, k, repr, inputs, &out_input_evals[1], rcp, out_proofs + nin);  // :112-113
+  if (rc == ZK_OK) rc = zk_kzg_g2_taus(k, out_g2_taus);
+  zk_kzg_free(k);
+  return rc;
+}
+
+int zk_gkr_circuit_verify_kzg(zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
+                              const zk_fe* output_poly, const zk_fe* coeffs, const uint8_t* ncoeffs,
+                              const zk_fe* claims, const zk_fe* opened_evals, const zk_g1* commitment,
+                              const zk_g1* proofs, const zk_g2* g2_taus, int* out_verified) {
+  std::vector<zk::Fe> chal;
+  uint32_t ninputs = 0;
+  int rc = guarded([&] {
+    require(output_poly && coeffs && ncoeffs && opened_evals && commitment && proofs && g2_taus && out_verified,
+            "null argument");
+    require(nlayers >= 1 && gates, "null argument");
+    ninputs = 2 * gates[0];
+    check_circuit(nlayers, gates, ops, ninputs);
+    require(nlayers == 1 || claims, "null argument");
+    *out_verified = gkr_circuit_verify_host<zk::Bls12_381Fr>(repr, nlayers, gates, ops, nullptr, ninputs, output_poly,
+                                                         coeffs, ncoeffs, claims, opened_evals, &chal)
+                        ? 1
+                        : 0;
+  });
+  if (rc != ZK_OK || !*out_verified) return rc;
+  // KZG::verify of both openings at (r_b, r_c), the verifier's own challenges (:155-175)
+  const uint32_t nin = lg2u(ninputs);
+  if (chal.size() != 2 * (size_t)nin) {  // the sum-check failed before the input layer
+    *out_verified = 0;
+    return ZK_OK;
+  }
+  std::vector<zk_fe> pts(2 * (size_t)nin);
+  for (size_t i = 0; i < pts.size(); ++i) pts[i] = out_repr<zk::Bls12_381Fr>(repr, chal[i]);
+  int okb = 0, okc = 0;
+  rc = zk_kzg_verify(repr, commitment, &opened_evals[0], proofs, nin, pts.data(), nin, g2_taus, &okb);
+  if (rc == ZK_OK) rc = zk_kzg_verify(repr, commitment, &opened_evals[1], proofs + nin, nin, pts.data() + nin, nin,
+                                      g2_taus, &okc);
+  *out_verified = rc == ZK_OK && okb && okc;
+  return rc;
 }
 
 }  // extern "C"

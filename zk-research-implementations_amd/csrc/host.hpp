@@ -208,6 +208,9 @@ struct zk_ctx {
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
   int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
   bool d0t = true;          // nv >= 11: rounds 0-2 in one pass, then steps that fold by three (ZK_D0T)
+  bool d0q = false;         // (d0t) rounds 0-3 in one pass, then one step that folds by four (ZK_D0Q; k_gkr_d0q, k_gkr_t33<.., 4>)
+  DevBuf wide;              // ZK_D0Q: [768 u64 limb accumulator][768 u64 all-reduce buffer] of the 729-limb step
+  uint64_t* h_wide = nullptr;  // pinned, device-mapped: its 729 round totals
   bool ttail = false;       // (d0t) triple steps to the end, the small ones in k_gkr_ttail (ZK_TTAIL; slower)
   bool dm = true;           // double steps with two pending challenges on the matrix cores (k_gkr_dm; ZK_DM=0: k_gkr_dround)
   uint64_t dm_min_quads = 1u << 17;  // ... when they have at least this many quads (ZK_DM_MIN_QUADS; smaller steps are latency-bound: k_gkr_dround)
@@ -396,6 +399,26 @@ inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   return s;
 }
 
+// The 729-limb step (k_gkr_d0q): its own accumulator, all-reduce buffer and
+// pinned totals (the shared ones hold <= 256 u64), the same counters and flag.
+inline void ensure_wide(zk_ctx* c) {
+  if (!c->h_wide) {
+    c->wide.ensure(2 * zk::kWideSlot * 8);
+    HIPCK(hipMemset(c->wide.p, 0, 2 * zk::kWideSlot * 8));
+    HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_wide), zk::kWideSlot * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(c->h_wide, 0, zk::kWideSlot * 8);
+  }
+  c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kWideSlot * 8);
+}
+inline zk::RoundSink make_sink_wide(zk_ctx* c, bool across_ranks) {
+  zk::RoundSink s = make_sink(c, across_ranks);
+  uint64_t* w = reinterpret_cast<uint64_t*>(c->wide.p);
+  s.accum = w;
+  if (s.dev_out) s.dev_out = w + zk::kWideSlot;
+  if (s.host_out) s.host_out = c->h_wide;
+  return s;
+}
+
 inline void wait_flag(zk_ctx* c, uint32_t tag) {
   const uint32_t* f = h_flag(c);
   uint64_t spins = 0;
@@ -432,6 +455,16 @@ inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks
   }
 }
 
+inline void enqueue_reduce_wide(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
+  if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
+    uint64_t* red = reinterpret_cast<uint64_t*>(c->wide.p) + zk::kWideSlot;
+    NCCLCK(ncclAllReduce(red, red, n, ncclUint64, ncclSum, c->nccl, c->stream));
+    c->stats.collectives += 1;
+    zk::k_publish<<<1, 256, 0, c->stream>>>(red, n, c->h_wide, h_flag(c), sk.tag);
+    HIPCK(hipGetLastError());
+  }
+}
+
 // product: the limb sums are sums of products of two Montgomery images (R^2
 // scale: REDC once); 17-word sums always are, 8-word sums are element sums
 // unless the kernel reduced product sums mod p in the block (k_gkr_d0t).
@@ -449,6 +482,23 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
     c->stats.collectives += 1;
   }
   for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w + L * k, L, L == 17 || product);
+}
+
+// the K x L limb sums of a 729-limb step (h_wide), summed over ranks when sharded
+template <class F, int K>
+void collect_wide(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
+  const bool multi = across_ranks && multi_rank(c);
+  const int n = K * L;
+  wait_flag(c, sk.tag);
+  if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) != 0)
+    fail(ZK_EDEVICE, "a pre-enqueued round kernel waited more than 1 s for its challenge");
+  std::vector<uint64_t> w(n);
+  for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_wide + i, __ATOMIC_RELAXED);
+  if (multi && c->comm == COMM_HOST) {
+    if (c->ar(c->user, w.data(), n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
+    c->stats.collectives += 1;
+  }
+  for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w.data() + L * k, L, true);
 }
 
 inline void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kSlotU64 * 8); }
@@ -505,14 +555,17 @@ struct PostR {
     __atomic_store_n(&s->tag, tag, __ATOMIC_RELEASE);
   }
   // the double-round slot: 24 self-tagged words (tag << 32 | limb), any order
-  void post2(const Fe& ra, const Fe& rb, const Fe& rab, uint32_t tag) {
+  void post2(const Fe& ra, const Fe& rb, const Fe& rab, uint32_t tag) { post4(ra, rb, rab, zk::Fe{}, tag); }
+  // four values (a fold by four: the pending challenges, oldest first); every word carries the tag
+  void post4(const Fe& ra, const Fe& rb, const Fe& rc, const Fe& rd, uint32_t tag) {
     note();
     zk::RPost* s = h_rpost(c);
     const uint64_t t = (uint64_t)tag << 32;
     for (int i = 0; i < 8; ++i) {
       __atomic_store_n(&s->w[i], t | ra.v[i], __ATOMIC_RELAXED);
       __atomic_store_n(&s->w[8 + i], t | rb.v[i], __ATOMIC_RELAXED);
-      __atomic_store_n(&s->w[16 + i], t | rab.v[i], __ATOMIC_RELAXED);
+      __atomic_store_n(&s->w[16 + i], t | rc.v[i], __ATOMIC_RELAXED);
+      __atomic_store_n(&s->w[24 + i], t | rd.v[i], __ATOMIC_RELAXED);
     }
   }
   ~PostR() {
@@ -569,7 +622,9 @@ enum {
   GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5, GS_D0T = 6, GS_T32 = 7, GS_T33 = 8,
   GS_TT = 9,     // one small triple step (k_gkr_ttail, one step per launch)
   GS_TTAIL = 10, // the small triple steps in one persistent kernel (k_gkr_ttail)
-  GS_HOST = 11   // the last rounds on the host, from the tables the persistent tail's last step hands over
+  GS_HOST = 11,  // the last rounds on the host, from the tables the persistent tail's last step hands over
+  GS_D0Q = 12,   // rounds 0-3 over the inputs (k_gkr_d0q)
+  GS_T43 = 13    // fold by the four pending challenges + three rounds (k_gkr_t33<F, 64, 4>)
 };
 
 // Host rounds (ZK_HOST_ROUNDS, default 4; only where the caller does not
@@ -633,19 +688,28 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   // latency-bound on tiny levels (~45 us per triple step against ~11 us per
   // double step of k_gkr_dtail).
   const bool d0t = c->dround && c->d0t && nv >= 11;
+  // ZK_D0Q: rounds 0-3 in the input pass (k_gkr_d0q) and a fold by four at
+  // level 4 (k_gkr_t33<F, 64, 4>: 1/16 of the tables written instead of 1/8),
+  // then the triple steps as after k_gkr_d0t from round 7. Needs >= 64
+  // octants at level 4 and no sharded cut before round 7.
+  bool d0q = d0t && c->d0q && !c->ttail && nv >= 15 && (gather_max == 0 || nv - 7 > gather_max);
   int nt = -1;
+  const int base = d0q ? 7 : 3;  // first round of the triple steps
   if (d0t && !c->ttail)
-    for (int k = 0; 3 + 3 * k + 8 <= (int)nv; ++k) {
-      const int R = (int)nv - 3 - 3 * k;
+    for (int k = 0; base + 3 * k + 8 <= (int)nv; ++k) {
+      const int R = (int)nv - base - 3 * k;
       if (R % 2 == 0 && (R >= 12 || nt < 0)) nt = k;
     }
+  if (d0q && nt < 0) d0q = false;
+  if (d0q) ensure_wide(c);  // (before anything of this phase is enqueued)
   const bool d0t_doubles = d0t && !c->ttail && nt >= 0;
   const bool d0t_triples = d0t && c->ttail;
   const bool d0 = !d0t_doubles && !d0t_triples && c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
-  if (nv >= 1) steps.push_back({d0t_doubles || d0t_triples ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0), 0, 0});
+  if (nv >= 1) steps.push_back({d0q ? GS_D0Q : (d0t_doubles || d0t_triples ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0)), 0, 0});
   if (d0t_doubles) {
-    for (int k = 0; k < nt; ++k) steps.push_back({GS_T33, 3u + 3u * k, 3});
-    steps.push_back({GS_T32, 3u + 3u * nt, 3});
+    if (d0q) steps.push_back({GS_T43, 4u, 4});
+    for (int k = 0; k < nt; ++k) steps.push_back({GS_T33, (uint32_t)base + 3u * k, 3});
+    steps.push_back({GS_T32, (uint32_t)base + 3u * nt, 3});
   }
   if (d0t_triples) {
     const int R = (int)nv - 3;
@@ -673,7 +737,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   if (d0t_triples) {
     // (the schedule above covers every round)
   } else if (c->dround) {
-    uint32_t i = d0t_doubles ? 5u + 3u * nt : (d0 ? 2 : 1);
+    uint32_t i = d0t_doubles ? (uint32_t)base + 2u + 3u * nt : (d0 ? 2 : 1);
     int np = d0t_doubles || d0 ? 2 : 1;  // challenges pending at the first double step
     if (!d0 && !d0t_doubles) {
       if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
@@ -750,7 +814,8 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   auto rounds_of = [&](const GStep& st) -> uint32_t {
     switch (st.kind) {
       case GS_DOUBLE: case GS_D0: case GS_T32: return 2;
-      case GS_D0T: case GS_T33: case GS_TT: return 3;
+      case GS_D0T: case GS_T33: case GS_TT: case GS_T43: return 3;
+      case GS_D0Q: return 4;
       case GS_DTAIL: return 2 * st.nd;
       case GS_TTAIL: return 3 * st.nd;
       case GS_TAIL: case GS_HOST: return nv - st.i;
@@ -783,7 +848,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
   std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
   int inbuf = -1;                        // work buffer holding cur (-1: the input tables)
-  Fe rz = zk::fe_zero<F>(), ra = zk::fe_zero<F>(), rb = zk::fe_zero<F>();  // last three challenges (oldest first)
+  Fe ry = zk::fe_zero<F>(), rz = ry, ra = ry, rb = ry;  // last four challenges (oldest first)
   auto out_tables = [&](uint64_t size, Fe* nx[4]) {
     const int ob = inbuf == 0 ? 1 : 0;
     Fe* w = c->work[ob].fe();
@@ -796,7 +861,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint32_t i = st.i;
     const uint64_t size = L >> i;  // table length in round i
     const uint64_t h = size / 2;   // pairs
-    sinks[i] = make_sink(c, across_ranks);
+    sinks[i] = st.kind == GS_D0Q ? make_sink_wide(c, across_ranks) : make_sink(c, across_ranks);
     if (c->block_trace && (int)si == c->block_trace_step) sinks[i].btrace = c->block_trace;
     const zk::RoundSink& sk = sinks[i];
     if (st.kind == GS_ROUND0) {
@@ -829,6 +894,16 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       const uint32_t grid = step_grid(c, res, std::max<uint64_t>(2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax))) & ~1u;
       launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
+      return;
+    }
+    if (st.kind == GS_D0Q) {  // rounds 0-3 over the input tables (size 16 H), nothing written
+      const uint64_t H = size / 16, nch = H / 32;
+      uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)c->num_cus, 2 * nch) & ~1u;  // one block per CU
+      if (c->grid_cap) grid = std::max<uint32_t>(2, std::min<uint32_t>(grid, c->grid_cap) & ~1u);
+      // a block takes at most kD0QDrain chunks (int32 tiles): more blocks than CUs beyond 24 variables
+      grid = std::max<uint32_t>(grid, (uint32_t)(2 * ((nch + zk::kD0QDrain - 1) / zk::kD0QDrain)));
+      launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0q<F>, grid, cur[0], cur[1], cur[2], cur[3], H, sk);
+      enqueue_reduce_wide(c, sk, across_ranks, zk::kD0QLimbs);
       return;
     }
     if (st.kind == GS_TT || st.kind == GS_TTAIL) {  // small triple steps (k_gkr_ttail)
@@ -879,7 +954,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (st.kind == GS_TT) enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
     }
-    if (st.kind == GS_T32 || st.kind == GS_T33) {  // fold level i-3 by three challenges to level i
+    if (st.kind == GS_T32 || st.kind == GS_T33 || st.kind == GS_T43) {  // fold level i-3 (i-4) by three (four) challenges to level i
       const uint64_t Q = size / 4;
       Fe* nx[4];
       out_tables(size, nx);
@@ -889,10 +964,25 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.relay = d_rpost(c);
         din.err = h_err(c);
         din.tag = rtags[si] = ++c->rtag;
+      } else if (st.kind == GS_T43) {
+        din.ra = ry;
+        din.rb = rz;
+        din.rab = ra;
+        din.r4 = rb;
       } else {
         din.ra = rz;
         din.rb = ra;
         din.rab = rb;  // carries r_{i-1} for this step
+      }
+      if (st.kind == GS_T43) {  // rounds i .. i+2 over level i's octants, folded from level i-4
+        const uint64_t O = size / 8, nch = O / 64;
+        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64, 4>);
+        const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
+        launch(c, ZK_K_GKR_T33, 17408.0 * O, 192.0 * O, zk::k_gkr_t33<F, 64, 4>, grid, cur[0], cur[1], cur[2], cur[3],
+               nx[0], nx[1], nx[2], nx[3], O, din, sk);
+        for (int t = 0; t < 4; ++t) cur[t] = nx[t];
+        enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
+        return;
       }
       if (st.kind == GS_T33) {  // rounds i .. i+2 over level i's octants: 27 moment sums
         const uint64_t O = size / 8;
@@ -1065,7 +1155,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     if (!pre || si + 1 >= ns) return;
     const GStep& nx = steps[si + 1];
     if (nx.kind == GS_HOST) return;
-    if (nx.kind == GS_T32 || nx.kind == GS_T33 || nx.kind == GS_TT || nx.kind == GS_TTAIL) {
+    if (nx.kind == GS_T43) {
+      post.post4(ry, rz, ra, rb, rtags[si + 1]);
+    } else if (nx.kind == GS_T32 || nx.kind == GS_T33 || nx.kind == GS_TT || nx.kind == GS_TTAIL) {
       post.post2(rz, ra, rb, rtags[si + 1]);
     } else if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
       if (nx.np == 2)
@@ -1078,6 +1170,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   };
   auto one_round = [&](uint32_t i, const Fe& e0, const Fe& e1, const Fe& e2) {
     claim = finish_round<F>(tr, e0, e1, e2, k0 + i, out, r);
+    ry = rz;
     rz = ra;
     ra = rb;
     rb = r;
@@ -1126,6 +1219,61 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     one_round(i0 + 2, Z[0], hfe_sub<F>(claim, Z[0]), at2w(Z[0], Z[1], Z[2]));
   };
+  // rounds i0 .. i0 + 3 from the 81 moment sums of k_gkr_d0q (27 t0 + 9 b + 3 c + d;
+  // t0: 0, 1, inf along the first variable, b, c, d: 0, 1, s as in three_rounds)
+  auto four_rounds = [&](uint32_t i0, bool first) {
+    using namespace zk;
+    Fe T[kD0QCats];
+    collect_wide<F, kD0QCats>(c, sinks[i0], across_ranks, 9, T);
+    for (int j = 0; j < 27; ++j) T[54 + j] = hfe_sub<F>(hfe_add<F>(T[j], T[27 + j]), T[54 + j]);  // X0 Y1 + X1 Y0
+    const Fe one = fe_one<F>(), two = hfe_add<F>(one, one), four = hfe_add<F>(two, two);
+    auto at2w = [&](const Fe (&m)[3]) { return hfe_sub<F>(hfe_add<F>(m[0], hfe_mul<F>(four, m[1])), hfe_mul<F>(two, m[2])); };
+    auto wts = [&](const Fe& t, Fe (&w)[3]) {
+      const Fe omt = hfe_sub<F>(one, t);
+      w[0] = hfe_mul<F>(omt, omt);
+      w[1] = hfe_mul<F>(t, t);
+      w[2] = hfe_mul<F>(t, omt);
+    };
+    auto dot3 = [&](const Fe (&w)[3], const Fe& x0, const Fe& x1, const Fe& x2) {  // one reduction
+      uint64_t acc[9] = {0};
+      h64::mac_wide(acc, h64::of(w[0]), h64::of(x0));
+      h64::mac_wide(acc, h64::of(w[1]), h64::of(x1));
+      h64::mac_wide(acc, h64::of(w[2]), h64::of(x2));
+      return wide_to_fe<F>(acc);
+    };
+    auto at = [&](int a, int b, int cc, int d) -> const Fe& { return T[27 * a + 9 * b + 3 * cc + d]; };
+    Fe S3[3][3][3], S2[3][3], U[3];  // sums over the trailing variables' hypercube points (moments 0 and 1)
+    for (int a = 0; a < 3; ++a) {
+      for (int b = 0; b < 3; ++b) {
+        for (int cc = 0; cc < 3; ++cc) S3[a][b][cc] = hfe_add<F>(at(a, b, cc, 0), at(a, b, cc, 1));
+        S2[a][b] = hfe_add<F>(S3[a][b][0], S3[a][b][1]);
+      }
+      U[a] = hfe_add<F>(S2[a][0], S2[a][1]);
+    }
+    one_round(i0, U[0], first ? U[1] : hfe_sub<F>(claim, U[0]), at2w(U));
+    Fe wa[3];
+    wts(r, wa);
+    Fe V[3];
+    for (int b = 0; b < 3; ++b) V[b] = dot3(wa, S2[0][b], S2[1][b], S2[2][b]);
+    one_round(i0 + 1, V[0], hfe_sub<F>(claim, V[0]), at2w(V));
+    Fe wb[3];
+    wts(r, wb);
+    Fe W2[3][3], Z[3];
+    for (int b = 0; b < 3; ++b)
+      for (int cc = 0; cc < 3; ++cc) W2[b][cc] = dot3(wa, S3[0][b][cc], S3[1][b][cc], S3[2][b][cc]);
+    for (int cc = 0; cc < 3; ++cc) Z[cc] = dot3(wb, W2[0][cc], W2[1][cc], W2[2][cc]);
+    one_round(i0 + 2, Z[0], hfe_sub<F>(claim, Z[0]), at2w(Z));
+    Fe wc[3];
+    wts(r, wc);
+    Fe W3[3][3][3], Wb[3][3], Q[3];
+    for (int b = 0; b < 3; ++b)
+      for (int cc = 0; cc < 3; ++cc)
+        for (int d = 0; d < 3; ++d) W3[b][cc][d] = dot3(wa, at(0, b, cc, d), at(1, b, cc, d), at(2, b, cc, d));
+    for (int cc = 0; cc < 3; ++cc)
+      for (int d = 0; d < 3; ++d) Wb[cc][d] = dot3(wb, W3[0][cc][d], W3[1][cc][d], W3[2][cc][d]);
+    for (int d = 0; d < 3; ++d) Q[d] = dot3(wc, Wb[0][d], Wb[1][d], Wb[2][d]);
+    one_round(i0 + 3, Q[0], hfe_sub<F>(claim, Q[0]), at2w(Q));
+  };
   // rounds i0 and i0 + 1 from a double step's eight product sums (the first
   // step of a phase, k_gkr_d0: nine, the ninth V11 for round 0's e1)
   auto two_rounds = [&](uint32_t i0, bool first = false) {
@@ -1167,6 +1315,12 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       pend = 2;
     } else if (st.kind == GS_D0T) {
       three_rounds(0, true);
+      pend = 3;
+    } else if (st.kind == GS_D0Q) {
+      four_rounds(0, true);
+      pend = 4;
+    } else if (st.kind == GS_T43) {
+      three_rounds(st.i, false);
       pend = 3;
     } else if (st.kind == GS_T32) {
       two_rounds(st.i);
@@ -1247,7 +1401,8 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     for (size_t si = 0; si < ns; ++si) {
       if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL || steps[si].kind == GS_HOST) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
-      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T;  // no challenge to wait for
+      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T ||
+                         steps[si].kind == GS_D0Q;  // no challenge to wait for
       const uint64_t rr = first ? row[0] : row[1];
       fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f"
               " (r->block 0 loop end %8.2f, ->publish %6.2f)\n", si, steps[si].kind, steps[si].i,
@@ -1497,14 +1652,16 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
     cur = nx;
   };
   PostR post{c};
+  enqueue(0);
+  tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps round 0 on the GPU
+  // The later rounds are pre-enqueued only after the hash: a round kernel that
+  // waited for its challenge across it would hit the device's 1 s wait guard
+  // (the hash of a 24-variable table's 512 MiB takes longer than that).
   if (pre)
-    for (uint32_t k = 0; k < n; ++k) {
+    for (uint32_t k = 1; k < n; ++k) {
       enqueue(k);
       post.last = rtags[k];
     }
-  else
-    enqueue(0);
-  tr->h.update(table_bytes, nbytes);  // serial Keccak overlaps the GPU
   for (uint32_t k = 0; k < n; ++k) {
     if (!pre && k > 0) enqueue(k);
     Fe s[2];

@@ -469,11 +469,11 @@ __device__ __forceinline__ void grid_finish(Sc& sc, const RoundSink& sk, uint32_
   ZK_STAMP(6);
 }
 
-// copy n <= 256 u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
+// copy n u64 (e.g. after an RCCL all-reduce) to pinned host memory + flag
 static __global__ void k_publish(const uint64_t* __restrict__ src, int n, uint64_t* host_out, uint32_t* host_flag,
                           uint32_t tag) {
-  if ((int)threadIdx.x < n)
-    __hip_atomic_store(host_out + threadIdx.x, src[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int i = (int)threadIdx.x; i < n; i += (int)blockDim.x)  // (n <= 768: the 729-limb step)
+    __hip_atomic_store(host_out + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(host_flag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -837,27 +837,30 @@ __global__ __launch_bounds__(kBlock) void k_gkr_tail(TailArgs a, RoundSink sink)
 // between the words is needed.
 // ---------------------------------------------------------------------------
 struct alignas(64) RPost {
-  uint64_t w[24];
-  uint64_t pad[8];
+  uint64_t w[32];  // up to four values; the two-round slot uses words 0-23
 };
 struct DIn {
   Fe ra, rb, rab;      // used as is when host == null
+  Fe r4;               // (four-challenge steps: the newest challenge; ra, rb, rab the older three)
   const RPost* host;   // pinned slot the host posts to, or null
   RPost* relay;        // device relay slot (used when gridDim > 1)
   uint32_t* err;       // pinned error word
   uint32_t tag;
 };
-__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab, bool relay) {
+template <int NV = 3>
+__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab, bool relay, Fe* r4 = nullptr) {
+  static_assert(NV == 3 || NV == 4, "three or four posted values");
   if (!in.host) {
     ra = in.ra;
     rb = in.rb;
     rab = in.rab;
+    if (NV == 4) *r4 = in.r4;
     return;
   }
-  __shared__ uint32_t s_w[24];
+  __shared__ uint32_t s_w[8 * NV];
   if (threadIdx.x < 64) {  // wave 0
     const uint32_t lane = threadIdx.x;
-    const bool mine = lane < 24;
+    const bool mine = lane < 8 * NV;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const bool direct = blockIdx.x == 0;
     uint64_t v = 0;
@@ -881,6 +884,7 @@ __device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& 
     ra.v[i] = s_w[i];
     rb.v[i] = s_w[8 + i];
     rab.v[i] = s_w[16 + i];
+    if (NV == 4) r4->v[i] = s_w[24 + i];
   }
 }
 

@@ -758,6 +758,259 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
 
 
 // ---------------------------------------------------------------------------
+// k_gkr_d0q: rounds 0-3 in ONE pass over the input tables (ZK_D0Q), so that
+// the first fold pass folds by four challenges and writes 1/16 of the tables
+// instead of 1/8 (DESIGN.md §3a'': the first fold pass is bound by its
+// read:write mix, and its writes are the lever). Along variable 0 a table
+// is written at the points 0, 1 and "infinity" (X(inf) = X1 - X0, the
+// leading coefficient of X(t) = X0 + t (X1 - X0); |X(inf)| < p keeps valid
+// signed digits for every field); per point t0 the products X(t0) Y(t0) over
+// the 8 x 8 corner pairs of variables 1-3 go to 27 moment tiles exactly as in
+// k_gkr_d0t: 81 tiles, indexed 27 t0 + 9 d1 + 3 d2 + d3 (d: 0 = X0 Y0,
+// 1 = X1 Y1, 2 = X0 Y1 + X1 Y0). The host (four_rounds) turns the t0 = inf
+// moment into the s moment: X0 Y1 + X1 Y0 = m0 + m1 - m_inf.
+// Block b serves product b & 1. Wave 3 is the producer: lane (table, group)
+// loads the group's 16 corners (two chunks in registers: the next chunk's
+// loads are in flight while this one is converted), forms the 8 inf values
+// and writes 24 digit rows per group into a double-buffered image
+// [t0][corner of variables 1-3][table][32 groups][32 B] (48 KiB per buffer);
+// waves 0-2 are the consumers of points t0 = 0, 1, inf: 64 MFMAs per chunk
+// into their 27 tiles (432 accumulator registers, one wave per SIMD). One
+// barrier per chunk: the producer fills buffer k & 1 while the consumers
+// multiply buffer (k - 1) & 1. int32 bound: a slot takes at most 8 MFMAs
+// per chunk (2^22), so a block takes at most kD0QDrain chunks (the host sizes
+// the grid: beyond 24 variables it exceeds one block per CU).
+// Output: 81 x 9 limb sums (grid_finish_wide).
+// ---------------------------------------------------------------------------
+constexpr int kD0QCats = 81;
+constexpr int kD0QLimbs = kD0QCats * 9;  // 729
+constexpr int kWideSlot = 768;           // per-block slot of grid_finish_wide (u64)
+constexpr uint32_t kD0QDrain = 256;      // chunks per block at most (the host sizes the grid; one drain at the end)
+static_assert(8ull * (1u << 19) * kD0QDrain <= (1ull << 30), "d0q tile bound");
+struct D0QEpi {
+  uint64_t w17[kD0QCats][17];
+  uint64_t tot[kWideSlot];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+};
+struct D0QScratch {
+  union {
+    uint8_t img[2][3][8][2][32][32];  // buffer, t0, corner (variables 1-3), table, group, digit row: 96 KiB
+    D0QEpi e;                         // epilogue (after the main loop)
+  };
+  unsigned long long T[kD0QCats][64];  // int64 anti-diagonal sums
+  uint32_t p2w[9][8];
+};
+
+// grid_finish for C > kBlock limb sums (sc.tot[0..C), every thread's share):
+// per-block slots of kWideSlot u64, the same two-level fan-in (or u64 atomics
+// for small grids) and publication as grid_finish.
+template <int C, class Sc>
+__device__ __forceinline__ void grid_finish_wide(Sc& sc, const RoundSink& sk) {
+  static_assert(C <= kWideSlot, "limb vector too long");
+  const uint32_t G = gridDim.x, t = threadIdx.x;
+  ZK_BLOCK_STAMP(sk, 1);
+  auto publish = [&]() {
+    for (uint32_t q = t; q < (uint32_t)C; q += kBlock) {
+      const uint64_t v = sc.tot[q];
+      if (sk.dev_out) sk.dev_out[q] = v;
+      if (sk.host_out) __hip_atomic_store(sk.host_out + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ZK_SINK_STAMP(sk, 2);
+    __syncthreads();  // every storing wave has drained before the flag
+    if (t == 0 && sk.host_flag) __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
+  if (G == 1) {
+    publish();
+    return;
+  }
+  if (G <= sk.atomic_max) {
+    for (uint32_t q = t; q < (uint32_t)C; q += kBlock)
+      __hip_atomic_fetch_add(sk.accum + q, sc.tot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) sc.am_last = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+    __syncthreads();
+    ZK_BLOCK_STAMP(sk, 2);
+    if (!sc.am_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t q = t; q < (uint32_t)C; q += kBlock)
+      sc.tot[q] = __hip_atomic_exchange(sk.accum + q, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    publish();
+    return;
+  }
+  auto sum_slots_wide = [&](uint32_t first, uint32_t stride, uint32_t count) {
+    for (uint32_t q = t; q < (uint32_t)C; q += kBlock) {
+      uint64_t s = 0;
+      uint32_t i = 0;
+      for (; i + 8 <= count; i += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld_u64_sc1(sk.partials + (uint64_t)(first + (i + u) * stride) * kWideSlot + q);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+      }
+      for (; i < count; ++i) s += ld_u64_sc1(sk.partials + (uint64_t)(first + i * stride) * kWideSlot + q);
+      sc.tot[q] = s;
+    }
+  };
+  const uint32_t shard = blockIdx.x & 7u, nshards = G < 8 ? G : 8u;
+  const uint32_t in_shard = (G - shard + 7u) / 8u;
+  for (uint32_t q = t; q < (uint32_t)C; q += kBlock) st_u64_sc1(sk.partials + (uint64_t)blockIdx.x * kWideSlot + q, sc.tot[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    sc.am_last = __hip_atomic_fetch_add(sk.counter + 32 * shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 in_shard - 1;
+  __syncthreads();
+  ZK_BLOCK_STAMP(sk, 2);
+  if (!sc.am_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  sum_slots_wide(shard, 8u, in_shard);
+  for (uint32_t q = t; q < (uint32_t)C; q += kBlock) st_u64_sc1(sk.partials + (uint64_t)(G + shard) * kWideSlot + q, sc.tot[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __hip_atomic_store(sk.counter + 32 * shard, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sc.am_last = __hip_atomic_fetch_add(sk.counter + 32 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nshards - 1;
+  }
+  __syncthreads();
+  if (!sc.am_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  sum_slots_wide(G, 1u, nshards);
+  if (t == 0) __hip_atomic_store(sk.counter + 32 * 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  publish();
+}
+
+// consumer: one chunk's 64 corner-pair products of point t0 into 27 tiles;
+// the tiles' register files are fixed here (16 in AGPRs, 11 in VGPRs): left to
+// itself the allocator spills whole tiles every chunk
+template <int SLOT>
+__device__ __forceinline__ void d0q_mfma(i32x16& acc, const i32x4& a, const i32x4& b) {
+  if constexpr (SLOT < 16)
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+template <int U, int V>
+__device__ __forceinline__ void d0q_pair(i32x16 (&acc)[27], const i32x4& fa, const i32x4& fb) {
+  constexpr int slot = 9 * moment_digit(U >> 2, V >> 2) + 3 * moment_digit((U >> 1) & 1, (V >> 1) & 1) +
+                       moment_digit(U & 1, V & 1);
+  d0q_mfma<slot>(acc[slot], fa, fb);
+}
+template <int U, int VH>
+__device__ __forceinline__ void d0q_row(i32x16 (&acc)[27], const i32x4& fa, const i32x4 (&fb)[4]) {
+  d0q_pair<U, 4 * VH + 0>(acc, fa, fb[0]);
+  d0q_pair<U, 4 * VH + 1>(acc, fa, fb[1]);
+  d0q_pair<U, 4 * VH + 2>(acc, fa, fb[2]);
+  d0q_pair<U, 4 * VH + 3>(acc, fa, fb[3]);
+}
+template <int VH>
+__device__ __forceinline__ void d0q_half(const uint8_t (*img)[2][32][32], i32x16 (&acc)[27]) {
+  i32x4 fb[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) fb[v] = tr_frag(&img[4 * VH + v][1][0][0]);
+  d0q_row<0, VH>(acc, tr_frag(&img[0][0][0][0]), fb);
+  d0q_row<1, VH>(acc, tr_frag(&img[1][0][0][0]), fb);
+  d0q_row<2, VH>(acc, tr_frag(&img[2][0][0][0]), fb);
+  d0q_row<3, VH>(acc, tr_frag(&img[3][0][0][0]), fb);
+  d0q_row<4, VH>(acc, tr_frag(&img[4][0][0][0]), fb);
+  d0q_row<5, VH>(acc, tr_frag(&img[5][0][0][0]), fb);
+  d0q_row<6, VH>(acc, tr_frag(&img[6][0][0][0]), fb);
+  d0q_row<7, VH>(acc, tr_frag(&img[7][0][0][0]), fb);
+}
+__device__ __forceinline__ void d0q_mfmas(const uint8_t (*img)[2][32][32], i32x16 (&acc)[27]) {
+  d0q_half<0>(img, acc);
+  d0q_half<1>(img, acc);
+}
+// tile -> the block's int64 anti-diagonal sums (categories 27 t0 + slot)
+__device__ __forceinline__ void d0q_drain(i32x16 (&acc)[27], unsigned long long (&T)[kD0QCats][64], uint32_t t0) {
+  // the MFMAs above are inline asm: the hazard recognizer does not see their
+  // result latency, so wait it out (>= 18 wait states for a 16-pass MFMA) before reading
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  const uint32_t l = threadIdx.x & 63, col = l & 31, h = l >> 5;
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      atomicAdd(&T[27 * t0 + i][row + col], (unsigned long long)(long long)acc[i][r]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one tile at a time (all 432 widened values would go live at once)
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(kBlock, 1) void k_gkr_d0q(const Fe* __restrict__ A, const Fe* __restrict__ S,
+                                                      const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t H,
+                                                      RoundSink sink) {
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
+  __shared__ D0QScratch sc;
+  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
+  for (uint32_t i = t; i < kD0QCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
+  stage_p2w<F>(sc.p2w);
+  const uint32_t pp = blockIdx.x & 1;
+  const uint64_t nch = H / 32, nb = gridDim.x >> 1, ch0 = blockIdx.x >> 1;
+  const uint64_t nk = ch0 < nch ? (nch - 1 - ch0) / nb + 1 : 0;  // this block's chunks: ch0 + k nb
+  __syncthreads();
+  if (w == 3) {  // producer: lane = (table, group)
+    const uint32_t tb = l >> 5, g = l & 31;
+    const Fe* __restrict__ X = tb ? (pp ? P : S) : (pp ? M : A);
+    // corner q = 8 u0 + (corner of variables 1-3). Pair q = corners q, 8 + q (X0, X1
+    // along variable 0) sits in cq[q]; once pair q of chunk k is converted its
+    // registers take pair q of chunk k + 1, so one chunk is always in flight
+    // (8 pairs, 128 VGPRs)
+    Fe cq[8][2];
+    auto load_pair = [&](uint64_t k, int q) {
+      const uint64_t j = (ch0 + k * nb) * 32 + g;
+      cq[q][0] = ld_fe(X, j + (uint64_t)q * H);
+      cq[q][1] = ld_fe(X, j + (uint64_t)(8 + q) * H);
+    };
+    if (nk > 0)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) load_pair(0, q);
+    for (uint64_t k = 0; k < nk; ++k) {
+      const uint32_t buf = (uint32_t)(k & 1);
+      const bool more = k + 1 < nk;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        Fe x0 = cq[q][0], x1 = cq[q][1];
+        if (more) load_pair(k + 1, q);
+        Fe d = sub256(x1, x0);  // X(inf) in (-p, p)
+        to_digits(d);
+        st_row(&sc.img[buf][2][q][tb][g][0], d);
+        to_digits(x0);
+        st_row(&sc.img[buf][0][q][tb][g][0], x0);
+        to_digits(x1);
+        st_row(&sc.img[buf][1][q][tb][g][0], x1);
+      }
+      __syncthreads();  // image k complete
+    }
+  } else {  // consumers: wave w multiplies point t0 = w
+    i32x16 acc[27];
+#pragma unroll
+    for (int i = 0; i < 27; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0;
+    for (uint64_t k = 0; k < nk; ++k) {  // nk <= kD0QDrain (the host sizes the grid)
+      __syncthreads();  // image k is complete
+      d0q_mfmas(sc.img[k & 1][w], acc);
+    }
+    d0q_drain(acc, sc.T, w);
+  }
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
+  ZK_BLOCK_STAMP(sink, 0);
+  __syncthreads();  // every drain is in T; the image is free for the epilogue
+  tiles_to_words<F, kD0QCats>(sc.T, sc.e.w17);
+  words_to_limbs9<F, kD0QCats>(sc.e.w17, sc.p2w, sc.e.tot);
+  __syncthreads();
+  grid_finish_wide<kD0QLimbs>(sc.e, sink);
+}
+
+// ---------------------------------------------------------------------------
 // k_gkr_dm3: the double step after k_gkr_d0t — THREE pending challenges
 // (ra, rb, rc) = (r_{i-3}, r_{i-2}, r_{i-1}). The level-(i-3) tables fold to
 // level i in one pass by the multilinear extension's own weights:
@@ -881,25 +1134,31 @@ struct T33Scratch {
   uint64_t pp[kBlock];
   uint32_t am_last;
   uint32_t p2w[9][8];  // 2^(32 (8 + k)) mod p, staged at kernel start for words_to_limbs9
-  Fe eqw[8];
+  Fe eqw[16];
 };
 
-template <class F, int OCT>
+// NP = 3: the fold by the three pending challenges (after k_gkr_d0t or a
+// previous triple step); NP = 4: by four (k_gkr_t43, after k_gkr_d0q): 16
+// inputs per output, K = 512, the 16 eq weights, and one fold's inputs in
+// flight instead of two (the same bytes), OCT 64 only.
+template <class F, int OCT, int NP = 3>
 __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
                                                       Fe* __restrict__ P2, uint64_t O, DIn din, RoundSink sink) {
-  Fe ra, rb, rc;
+  static_assert(NP == 3 || (NP == 4 && OCT == 64), "fold by three, or by four with 64-octant chunks");
+  constexpr int NI = 1 << NP;  // inputs per output
+  Fe ra, rb, rc, rd;
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
   const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
   Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
   const uint64_t nch = O / OCT, h8 = 8 * O;  // level-i tables hold 8 O elements
   // fold f's inputs: OCT 64: corner f of octants ch*64 + l; OCT 32: corner 2f + hh of octants ch*32 + ql
-  auto in_at = [&](uint64_t ch, int f, Fe (&x)[8]) {
+  auto in_at = [&](uint64_t ch, int f, Fe (&x)[NI]) {
     const uint64_t e = OCT == 64 ? ch * 64 + l + (uint64_t)f * O : ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
+    for (int k = 0; k < NI; ++k) x[k] = ld_fe(X, e + k * h8);
   };
   // inputs two folds ahead (one wave per SIMD: the loads in flight are what
   // hides HBM latency). OCT 64: the first two folds' inputs (written by the
@@ -908,34 +1167,41 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   // Block 0's wave 0 polls the host for the challenges and relays them to
   // every block: its poll would wait behind these loads (vmcnt is in order),
   // so it loads after the challenges arrive.
-  Fe nx[8], nx2[8];
+  Fe nx[NI], nx2[NP == 3 ? NI : 1];
   const bool early = OCT == 64 && (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
   if (early) {
     in_at(blockIdx.x, 0, nx);
-    in_at(blockIdx.x, 1, nx2);
+    if constexpr (NP == 3) in_at(blockIdx.x, 1, nx2);
   }
-  block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc for this step
+  // the third word group carries rc for this step; a fold by four reads a fourth group
+  if constexpr (NP == 4)
+    block_get_rs<4>(din, ra, rb, rc, gridDim.x > 1, &rd);
+  else
+    block_get_rs(din, ra, rb, rc, gridDim.x > 1);
   if (OCT == 64 && !early && (uint64_t)blockIdx.x < nch) {
     in_at(blockIdx.x, 0, nx);
-    in_at(blockIdx.x, 1, nx2);
+    if constexpr (NP == 3) in_at(blockIdx.x, 1, nx2);
   }
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ T33Scratch sc;
-  if (t < 8) {  // eq((ra, rb, rc), c), c = 4a + 2b + c0
+  if (t < (uint32_t)NI) {  // eq(r, c), the oldest pending challenge on c's top bit: c = 4a + 2b + c0 (+ d below)
     const Fe one = fe_one<F>();
-    const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
-    const Fe fc = (t & 1) ? rc : fe_sub<F>(one, rc);
-    sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
+    const uint32_t c3 = NP == 4 ? t >> 1 : t;  // the three older challenges' bits
+    const Fe fa = (c3 & 4) ? ra : fe_sub<F>(one, ra), fb = (c3 & 2) ? rb : fe_sub<F>(one, rb);
+    const Fe fc = (c3 & 1) ? rc : fe_sub<F>(one, rc);
+    Fe e = fe_mul<F>(fe_mul<F>(fa, fb), fc);
+    if constexpr (NP == 4) e = fe_mul<F>(e, (t & 1) ? rd : fe_sub<F>(one, rd));
+    sc.eqw[t] = e;
   }
   for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
   stage_p2w<F>(sc.p2w);
   __syncthreads();
   uint8_t(*wimg)[32][32] = reinterpret_cast<uint8_t(*)[32][32]>(&sc.img[0][0][0][0][0]);
-  dm_row<F>(wimg[t >> 5][t & 31], fe_mul<F>(sc.eqw[t >> 5], p2dig<F>(t & 31)));
+  for (uint32_t q = t; q < 32u * NI; q += kBlock) dm_row<F>(wimg[q >> 5][q & 31], fe_mul<F>(sc.eqw[q >> 5], p2dig<F>(q & 31)));
   __syncthreads();
-  i32x4 wf[8];
+  i32x4 wf[NI];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
+  for (int c = 0; c < NI; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
   __syncthreads();
   i32x16 acc[9];
 #pragma unroll
@@ -947,17 +1213,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
-      Fe x[8];
+      Fe x[NI];
+      if constexpr (NP == 4) {  // one fold ahead (16 inputs in flight)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        x[k] = nx[k];
-        nx[k] = nx2[k];
+        for (int k = 0; k < NI; ++k) x[k] = nx[k];
+        if (f < 7)
+          in_at(ch, f + 1, nx);
+        else if (ch + gridDim.x < nch)
+          in_at(ch + gridDim.x, 0, nx);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+          x[k] = nx[k];
+          nx[k] = nx2[k];
+        }
+        if (f < 6)
+          in_at(ch, f + 2, nx2);
+        else if (ch + gridDim.x < nch)
+          in_at(ch + gridDim.x, f - 6, nx2);
       }
-      if (f < 6)
-        in_at(ch, f + 2, nx2);
-      else if (ch + gridDim.x < nch)
-        in_at(ch + gridDim.x, f - 6, nx2);
-      const Fe z = dm3_fold<F>(x, wf);
+      const Fe z = dm3_fold<F, NP>(x, wf);
       st_fold(X2, ch * 64 + l + (uint64_t)f * O, z);
       dm_row<F>(img[f][w][l], z);
     }

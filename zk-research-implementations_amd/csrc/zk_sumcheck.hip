@@ -50,6 +50,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_DTAIL")) c->dtail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DM")) c->dm = atoi(e) != 0;
     if (const char* e = getenv("ZK_D0T")) c->d0t = atoi(e) != 0;
+    if (const char* e = getenv("ZK_D0Q")) c->d0q = atoi(e) != 0;
     if (const char* e = getenv("ZK_TTAIL")) c->ttail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DM_MIN_QUADS")) c->dm_min_quads = strtoull(e, nullptr, 0);
     if (const char* e = getenv("ZK_D0")) c->d0 = atoi(e);
@@ -106,6 +107,8 @@ void zk_ctx_destroy(zk_ctx* c) {
   if (c->tail_trace) (void)hipHostFree(c->tail_trace);
   if (c->block_trace) (void)hipHostFree(c->block_trace);
   c->small.release();
+  c->wide.release();
+  if (c->h_wide) (void)hipHostFree(c->h_wide);
   c->gbuf.release();
   for (auto& b : c->msm) b.release();
   for (auto& b : c->scan_tmp) b.release();

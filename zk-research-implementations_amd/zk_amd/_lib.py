@@ -78,6 +78,8 @@ SIGNATURES = {
     "zk_gkr_circuit_rounds": (I, [U32, P, C.POINTER(U32)]),
     "zk_gkr_circuit_prove": (I, [P, I, I, U32, P, P, P, U32, P, P, P, P, P, P]),
     "zk_gkr_circuit_verify": (I, [I, I, U32, P, P, P, U32, P, P, P, P, P, C.POINTER(C.c_int)]),
+    "zk_gkr_circuit_prove_kzg": (I, [P, I, U32, P, P, P, U32, P, P, P, P, P, P, P, P, P, P]),
+    "zk_gkr_circuit_verify_kzg": (I, [I, U32, P, P, P, P, P, P, P, P, P, P, C.POINTER(C.c_int)]),
     "zk_kzg_setup": (I, [P, I, P, U32, C.POINTER(C.c_void_p)]),
     "zk_kzg_free": (None, [P]),
     "zk_kzg_lagrange_basis": (I, [P, P, U32, P]),

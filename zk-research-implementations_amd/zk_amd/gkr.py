@@ -2,10 +2,15 @@
 gkr/src/gkr_protocol.rs) over the C ABI: a layered circuit, `prove` (circuit
 evaluation, per-layer tables and sum-checks on the GPU) and `verify` (host).
 
-Differences from the reference, all forced by SURVEY.md 8(f2)/(f3):
-* the input layer is not committed with KZG (row f3); the proof carries the
-  two input-MLE evaluations KZG::open would return, and `verify` recomputes
-  them from the inputs when they are given;
+Differences from the reference:
+* the input layer's KZG step (gkr_protocol.rs:92-118) runs when `prove` is
+  given taus (BLS12-381 Fr, the reference's KZG field): the proof then carries
+  `input_proof` (commitment, both get_proofs, the opened values, the G2 taus)
+  and `verify` checks it with two KZG::verify pairings (:155-175). The
+  reference draws the taus from entropy (:97-103); they are the caller's here
+  so proofs are reproducible. Without taus the proof carries only the two
+  input-MLE evaluations KZG::open would return, and `verify` recomputes them
+  from the inputs when they are given;
 * only the circuit shape for which the reference's table sizes agree is
   accepted (binary tree, powers of two, 1- or 2-gate output layer);
   anything else raises ValueError (the reference panics or mis-sizes).
@@ -56,12 +61,21 @@ class Circuit:  # gkr_circuit.rs:107-144
 
 
 @dataclass
-class GkrCircuitProof:  # gkr_protocol.rs:23-29 (input_proof -> input_evaluations)
+class KzgProof:  # gkr_protocol.rs:15-21
+    commitment: tuple | None              # G1 affine (x, y), None = infinity
+    proof: tuple[list, list]              # get_proof at r_b, at r_c (nvars G1 points each)
+    opened_evals: tuple[int, int]         # KZG::open at r_b, r_c
+    g2_taus: list                         # kzg_setup.g2_taus
+
+
+@dataclass
+class GkrCircuitProof:  # gkr_protocol.rs:23-29
     output_poly: list[int]
     proof_polynomials: list[list[UnivariatePoly]]  # per layer, output layer first
     claimed_evaluations: list[tuple[int, int]]
     input_evaluations: tuple[int, int]
     random_challenges: list[list[int]]
+    input_proof: KzgProof | None = None
 
 
 def _rounds(gates: np.ndarray) -> int:
@@ -70,8 +84,11 @@ def _rounds(gates: np.ndarray) -> int:
     return n.value
 
 
-def prove(circuit: Circuit, inputs: list[int], ctx: Context | None = None) -> GkrCircuitProof:  # :31-126
+def prove(circuit: Circuit, inputs: list[int], ctx: Context | None = None,
+          taus: list[int] | None = None) -> GkrCircuitProof:  # :31-126
     ctx = ctx or default_context()
+    if taus is not None:
+        return _prove_kzg(circuit, inputs, ctx, taus)
     gates, ops = circuit._abi()
     total = _rounds(gates)
     L = len(gates)
@@ -95,6 +112,60 @@ def prove(circuit: Circuit, inputs: list[int], ctx: Context | None = None) -> Gk
                            tuple(to_ints(ins)), chal)
 
 
+def _prove_kzg(circuit: Circuit, inputs: list[int], ctx: Context, taus: list[int]) -> GkrCircuitProof:
+    from .kzg import _g2_points, _points
+
+    if circuit.field != Field.BLS12_381_FR:
+        raise ValueError("the input layer's KZG commitment is over BLS12-381 (kzg.rs:3): use Field.BLS12_381_FR")
+    gates, ops = circuit._abi()
+    total = _rounds(gates)
+    L = len(gates)
+    nin = len(inputs).bit_length() - 1
+    if len(taus) != nin:
+        raise ValueError(f"need {nin} taus (one per input variable)")
+    outp = np.zeros((2, 4), np.uint64)
+    coeffs = np.zeros((total, 3, 4), np.uint64)
+    nco = np.zeros(total, np.uint8)
+    ch = np.zeros((total, 4), np.uint64)
+    claims = np.zeros((max(2 * (L - 1), 1), 4), np.uint64)
+    ins = np.zeros((2, 4), np.uint64)
+    com = np.zeros((1, 12), np.uint64)
+    prf = np.zeros((max(2 * nin, 1), 12), np.uint64)
+    g2 = np.zeros((max(nin, 1), 24), np.uint64)
+    x = as_limbs([int(v) for v in inputs])
+    _call(lib().zk_gkr_circuit_prove_kzg(ctx.h, REPR_CANONICAL, L, ptr(gates), ptr(ops), ptr(x), len(inputs),
+                                         ptr(as_limbs([int(t) for t in taus])), ptr(outp), ptr(coeffs), ptr(nco),
+                                         ptr(ch), ptr(claims), ptr(ins), ptr(com), ptr(prf), ptr(g2)))
+    polys, chal, k0 = [], [], 0
+    for layer in reversed(range(L)):
+        nv = 2 * (2 * int(gates[layer])).bit_length() - 2
+        polys.append([UnivariatePoly(to_ints(coeffs[k, : nco[k]]), circuit.field) for k in range(k0, k0 + nv)])
+        chal.append(to_ints(ch[k0: k0 + nv]))
+        k0 += nv
+    cl = to_ints(claims[: 2 * (L - 1)])
+    opened = tuple(to_ints(ins))
+    pts = _points(prf[: 2 * nin])
+    kp = KzgProof(_points(com)[0], (pts[:nin], pts[nin:]), opened, _g2_points(g2[:nin]))
+    return GkrCircuitProof(to_ints(outp), polys, [(cl[2 * i], cl[2 * i + 1]) for i in range(L - 1)], opened, chal, kp)
+
+
+def _verify_kzg(proof: GkrCircuitProof, circuit: Circuit, gates, ops, coeffs, nco, claims) -> bool:
+    from .kzg import _g1_array, _g2_array
+
+    kp = proof.input_proof
+    nin = (2 * int(gates[0])).bit_length() - 1
+    if circuit.field != Field.BLS12_381_FR or len(kp.proof) != 2 or any(len(q) != nin for q in kp.proof) \
+            or len(kp.g2_taus) != nin:
+        return False
+    ok = C.c_int(0)
+    _call(lib().zk_gkr_circuit_verify_kzg(REPR_CANONICAL, len(gates), ptr(gates), ptr(ops),
+                                          ptr(as_limbs(proof.output_poly)), ptr(coeffs), ptr(nco), ptr(claims),
+                                          ptr(as_limbs(list(kp.opened_evals))), ptr(_g1_array([kp.commitment])),
+                                          ptr(_g1_array(list(kp.proof[0]) + list(kp.proof[1]))),
+                                          ptr(_g2_array(kp.g2_taus)), C.byref(ok)))
+    return bool(ok.value)
+
+
 def verify(proof: GkrCircuitProof, circuit: Circuit, inputs: list[int] | None = None) -> bool:  # :128-227
     gates, ops = circuit._abi()
     total = _rounds(gates)
@@ -115,6 +186,8 @@ def verify(proof: GkrCircuitProof, circuit: Circuit, inputs: list[int] | None = 
     if len(cl) != 2 * (L - 1):
         return False
     claims = as_limbs(cl) if cl else np.zeros((1, 4), np.uint64)
+    if proof.input_proof is not None:  # the reference's verifier: KZG checks, no inputs needed
+        return _verify_kzg(proof, circuit, gates, ops, coeffs, nco, claims)
     x = as_limbs([int(v) for v in inputs]) if inputs is not None else None
     ok = C.c_int(0)
     _call(lib().zk_gkr_circuit_verify(int(circuit.field), REPR_CANONICAL, L, ptr(gates), ptr(ops),
