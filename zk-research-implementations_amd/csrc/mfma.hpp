@@ -769,15 +769,15 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
 // k_gkr_d0t: 81 tiles, indexed 27 t0 + 9 d1 + 3 d2 + d3 (d: 0 = X0 Y0,
 // 1 = X1 Y1, 2 = X0 Y1 + X1 Y0). The host (four_rounds) turns the t0 = inf
 // moment into the s moment: X0 Y1 + X1 Y0 = m0 + m1 - m_inf.
-// Block b serves product b & 1. Wave 3 is the producer: lane (table, group)
-// loads the group's 16 corners (two chunks in registers: the next chunk's
-// loads are in flight while this one is converted), forms the 8 inf values
-// and writes 24 digit rows per group into a double-buffered image
-// [t0][corner of variables 1-3][table][32 groups][32 B] (48 KiB per buffer);
-// waves 0-2 are the consumers of points t0 = 0, 1, inf: 64 MFMAs per chunk
-// into their 27 tiles (432 accumulator registers, one wave per SIMD). One
-// barrier per chunk: the producer fills buffer k & 1 while the consumers
-// multiply buffer (k - 1) & 1. int32 bound: a slot takes at most 8 MFMAs
+// Block b serves product b & 1. Lane (table, group) of every wave loads two
+// of the group's eight corner pairs (the next chunk's loads in flight while
+// this one is converted), forms the inf values and writes 3 digit rows per
+// pair into a double-buffered image [t0][corner of variables 1-3][table][32
+// groups][32 B] (48 KiB per buffer); the chunk's 192 products are split over
+// the four waves (48 each, at most 21 tiles, d0q_group), one wave per SIMD.
+// (A first version had one wave convert all eight pairs for three waves of
+// 27 tiles: issue-bound, 0.8 ms per pass at 24 variables.) One barrier per
+// chunk: the waves fill buffer k & 1 and multiply buffer (k - 1) & 1. int32 bound: a slot takes at most 8 MFMAs
 // per chunk (2^22), so a block takes at most kD0QDrain chunks (the host sizes
 // the grid: beyond 24 variables it exceeds one block per CU).
 // Output: 81 x 9 limb sums (grid_finish_wide).
@@ -884,63 +884,211 @@ __device__ __forceinline__ void grid_finish_wide(Sc& sc, const RoundSink& sk) {
   publish();
 }
 
-// consumer: one chunk's 64 corner-pair products of point t0 into 27 tiles;
-// the tiles' register files are fixed here (16 in AGPRs, 11 in VGPRs): left to
-// itself the allocator spills whole tiles every chunk
+// The 192 products of a chunk (64 corner pairs (U, V) of variables 1-3 per
+// point t0) and the 81 tiles they feed are split over the four waves so that
+// every wave takes 48 products and at most 21 tiles, leaving registers for
+// two of the chunk's eight pairs of loads per lane: wave w < 3 takes point
+// t0 = w except the tiles with d1 = s, d2 != s (21 tiles: local group
+// g = 3 d1 + d2 for d1 < 2, g = 6 for (s, s)); wave 3 takes exactly those
+// (t0, s, d2 < 2) tiles of every point (18 tiles: g = 2 t0 + d2). Local tile
+// 3 g + d3. The tiles' register files are fixed here (the first 16 in AGPRs,
+// the rest in VGPRs): left to itself the allocator spills whole tiles every
+// chunk, and a spill of an inline-asm MFMA's result would race the MFMA.
 template <int SLOT>
 __device__ __forceinline__ void d0q_mfma(i32x16& acc, const i32x4& a, const i32x4& b) {
+#if defined(ZK_D0Q_BUILTIN)
+  acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+  return;
+#endif
   if constexpr (SLOT < 16)
     asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else
     asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
-template <int U, int V>
-__device__ __forceinline__ void d0q_pair(i32x16 (&acc)[27], const i32x4& fa, const i32x4& fb) {
-  constexpr int slot = 9 * moment_digit(U >> 2, V >> 2) + 3 * moment_digit((U >> 1) & 1, (V >> 1) & 1) +
-                       moment_digit(U & 1, V & 1);
-  d0q_mfma<slot>(acc[slot], fa, fb);
+__host__ __device__ constexpr int d0q_group(int role, int t0, int d1, int d2) {
+  return role == 0 ? (d1 < 2 ? 3 * d1 + d2 : (d2 == 2 ? 6 : -1)) : (d1 == 2 && d2 < 2 ? 2 * t0 + d2 : -1);
 }
-template <int U, int VH>
-__device__ __forceinline__ void d0q_row(i32x16 (&acc)[27], const i32x4& fa, const i32x4 (&fb)[4]) {
-  d0q_pair<U, 4 * VH + 0>(acc, fa, fb[0]);
-  d0q_pair<U, 4 * VH + 1>(acc, fa, fb[1]);
-  d0q_pair<U, 4 * VH + 2>(acc, fa, fb[2]);
-  d0q_pair<U, 4 * VH + 3>(acc, fa, fb[3]);
+template <int ROLE, int T0, int U, int V, int NT>
+__device__ __forceinline__ void d0q_prod(i32x16 (&acc)[NT], const i32x4& fa, const i32x4& fb) {
+  constexpr int d1 = moment_digit(U >> 2, V >> 2), d2 = moment_digit((U >> 1) & 1, (V >> 1) & 1);
+  constexpr int g = d0q_group(ROLE, T0, d1, d2);
+  if constexpr (g >= 0) {
+    constexpr int slot = 3 * g + moment_digit(U & 1, V & 1);
+    d0q_mfma<slot>(acc[slot], fa, fb);
+  }
 }
-template <int VH>
-__device__ __forceinline__ void d0q_half(const uint8_t (*img)[2][32][32], i32x16 (&acc)[27]) {
+template <int ROLE, int T0, int U, int VH, int NT>
+__device__ __forceinline__ void d0q_row(i32x16 (&acc)[NT], const i32x4& fa, const i32x4 (&fb)[4]) {
+  d0q_prod<ROLE, T0, U, 4 * VH + 0>(acc, fa, fb[0]);
+  d0q_prod<ROLE, T0, U, 4 * VH + 1>(acc, fa, fb[1]);
+  d0q_prod<ROLE, T0, U, 4 * VH + 2>(acc, fa, fb[2]);
+  d0q_prod<ROLE, T0, U, 4 * VH + 3>(acc, fa, fb[3]);
+}
+// Wave w < 3 (ROLE 0): the products of its point's image img = [corner][table]
+// [32][32] with Y corners 4 VH .. 4 VH + 3: rows with u1 = VH take 4 products,
+// the others 2; X fragments are read two rows ahead (three in registers) so
+// a 2-product row does not wait for its read (the MFMAs are volatile asm: the
+// scheduler does not hoist reads above them on its own).
+template <int VH, int NT>
+__device__ __forceinline__ void d0q_half(const uint8_t (*img)[2][32][32], i32x16 (&acc)[NT]) {
   i32x4 fb[4];
 #pragma unroll
   for (int v = 0; v < 4; ++v) fb[v] = tr_frag(&img[4 * VH + v][1][0][0]);
-  d0q_row<0, VH>(acc, tr_frag(&img[0][0][0][0]), fb);
-  d0q_row<1, VH>(acc, tr_frag(&img[1][0][0][0]), fb);
-  d0q_row<2, VH>(acc, tr_frag(&img[2][0][0][0]), fb);
-  d0q_row<3, VH>(acc, tr_frag(&img[3][0][0][0]), fb);
-  d0q_row<4, VH>(acc, tr_frag(&img[4][0][0][0]), fb);
-  d0q_row<5, VH>(acc, tr_frag(&img[5][0][0][0]), fb);
-  d0q_row<6, VH>(acc, tr_frag(&img[6][0][0][0]), fb);
-  d0q_row<7, VH>(acc, tr_frag(&img[7][0][0][0]), fb);
+  i32x4 f0 = tr_frag(&img[0][0][0][0]), f1 = tr_frag(&img[1][0][0][0]), f2 = tr_frag(&img[2][0][0][0]);
+  d0q_row<0, 0, 0, VH>(acc, f0, fb);
+  f0 = tr_frag(&img[3][0][0][0]);
+  d0q_row<0, 0, 1, VH>(acc, f1, fb);
+  f1 = tr_frag(&img[4][0][0][0]);
+  d0q_row<0, 0, 2, VH>(acc, f2, fb);
+  f2 = tr_frag(&img[5][0][0][0]);
+  d0q_row<0, 0, 3, VH>(acc, f0, fb);
+  f0 = tr_frag(&img[6][0][0][0]);
+  d0q_row<0, 0, 4, VH>(acc, f1, fb);
+  f1 = tr_frag(&img[7][0][0][0]);
+  d0q_row<0, 0, 5, VH>(acc, f2, fb);
+  d0q_row<0, 0, 6, VH>(acc, f0, fb);
+  d0q_row<0, 0, 7, VH>(acc, f1, fb);
 }
-__device__ __forceinline__ void d0q_mfmas(const uint8_t (*img)[2][32][32], i32x16 (&acc)[27]) {
-  d0q_half<0>(img, acc);
-  d0q_half<1>(img, acc);
+// Wave 3 (ROLE 1): stage (T0, VH) = the products X_U Y_V of point T0 with
+// v1 = VH, u1 = 1 - VH, u2 = v2 (8 products over 4 X and 4 Y fragments);
+// img3 = the whole buffer [t0][corner][table][32][32]. A stage's fragments are
+// read while the previous stage multiplies (two register sets).
+struct D0QFrags {
+  i32x4 a[4], b[4];
+};
+template <int T0, int VH>
+__device__ __forceinline__ void d0q_stage_load(const uint8_t (*img3)[8][2][32][32], D0QFrags& f) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) f.a[r] = tr_frag(&img3[T0][4 * (1 - VH) + r][0][0][0]);
+#pragma unroll
+  for (int v = 0; v < 4; ++v) f.b[v] = tr_frag(&img3[T0][4 * VH + v][1][0][0]);
 }
-// tile -> the block's int64 anti-diagonal sums (categories 27 t0 + slot)
-__device__ __forceinline__ void d0q_drain(i32x16 (&acc)[27], unsigned long long (&T)[kD0QCats][64], uint32_t t0) {
+template <int T0, int VH, int R, int NT>
+__device__ __forceinline__ void d0q_stage_row(i32x16 (&acc)[NT], const D0QFrags& f) {
+  d0q_prod<1, T0, 4 * (1 - VH) + R, 4 * VH + 2 * (R >> 1)>(acc, f.a[R], f.b[2 * (R >> 1)]);
+  d0q_prod<1, T0, 4 * (1 - VH) + R, 4 * VH + 2 * (R >> 1) + 1>(acc, f.a[R], f.b[2 * (R >> 1) + 1]);
+}
+template <int T0, int VH, int NT>
+__device__ __forceinline__ void d0q_stage(i32x16 (&acc)[NT], const D0QFrags& f) {
+  d0q_stage_row<T0, VH, 0>(acc, f);
+  d0q_stage_row<T0, VH, 1>(acc, f);
+  d0q_stage_row<T0, VH, 2>(acc, f);
+  d0q_stage_row<T0, VH, 3>(acc, f);
+}
+template <int NT>
+__device__ __forceinline__ void d0q_role1(const uint8_t (*img3)[8][2][32][32], i32x16 (&acc)[NT]) {
+  D0QFrags f0, f1;
+  d0q_stage_load<0, 0>(img3, f0);
+  d0q_stage_load<0, 1>(img3, f1);
+  d0q_stage<0, 0>(acc, f0);
+  d0q_stage_load<1, 0>(img3, f0);
+  d0q_stage<0, 1>(acc, f1);
+  d0q_stage_load<1, 1>(img3, f1);
+  d0q_stage<1, 0>(acc, f0);
+  d0q_stage_load<2, 0>(img3, f0);
+  d0q_stage<1, 1>(acc, f1);
+  d0q_stage_load<2, 1>(img3, f1);
+  d0q_stage<2, 0>(acc, f0);
+  d0q_stage<2, 1>(acc, f1);
+}
+// local tile i of a wave -> category 27 t0 + 9 d1 + 3 d2 + d3
+__device__ __forceinline__ uint32_t d0q_cat(int role, uint32_t w, int i) {
+  const int g = i / 3, d3 = i % 3;
+  if (role == 0) {
+    const int d1 = g < 6 ? g / 3 : 2, d2 = g < 6 ? g % 3 : 2;
+    return 27u * w + (uint32_t)(9 * d1 + 3 * d2 + d3);
+  }
+  return (uint32_t)(27 * (g >> 1) + 18 + 3 * (g & 1) + d3);
+}
+// tiles -> the block's int64 anti-diagonal sums
+template <int ROLE, int NT>
+__device__ __forceinline__ void d0q_drain(i32x16 (&acc)[NT], unsigned long long (&T)[kD0QCats][64], uint32_t w) {
   // the MFMAs above are inline asm: the hazard recognizer does not see their
   // result latency, so wait it out (>= 18 wait states for a 16-pass MFMA) before reading
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
   const uint32_t l = threadIdx.x & 63, col = l & 31, h = l >> 5;
 #pragma unroll
-  for (int i = 0; i < 27; ++i) {
+  for (int i = 0; i < NT; ++i) {
+    const uint32_t cat = d0q_cat(ROLE, w, i);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      atomicAdd(&T[27 * t0 + i][row + col], (unsigned long long)(long long)acc[i][r]);
+      atomicAdd(&T[cat][row + col], (unsigned long long)(long long)acc[i][r]);
     }
-    __builtin_amdgcn_sched_barrier(0);  // one tile at a time (all 432 widened values would go live at once)
+    __builtin_amdgcn_sched_barrier(0);  // one tile at a time (all widened values would go live at once)
   }
+}
+
+// pair q of group j (corners q and 8 + q along variable 0) of one table
+__device__ __forceinline__ void d0q_load(const Fe* __restrict__ X, uint64_t j, uint64_t H, int q, Fe (&x)[2]) {
+  x[0] = ld_fe(X, j + (uint64_t)q * H);
+  x[1] = ld_fe(X, j + (uint64_t)(8 + q) * H);
+}
+// the pair's three digit rows: t0 = 0, 1, inf (X(inf) = X1 - X0 in (-p, p))
+__device__ __forceinline__ void d0q_put(uint8_t (*img)[8][2][32][32], int q, uint32_t tb, uint32_t g, Fe (&x)[2]) {
+  Fe d = sub256(x[1], x[0]);
+  to_digits(d);
+  st_row(&img[2][q][tb][g][0], d);
+  to_digits(x[0]);
+  st_row(&img[0][q][tb][g][0], x[0]);
+  to_digits(x[1]);
+  st_row(&img[1][q][tb][g][0], x[1]);
+}
+
+// One wave's main loop: lane (table tb, group g) converts pairs 2w, 2w + 1 of
+// every chunk (the next chunk's loads in flight while this one is converted)
+// into image k (buffer k & 1) while the wave multiplies image k - 1; one
+// barrier per iteration (nk + 1 iterations for every wave).
+template <int ROLE>
+__device__ __forceinline__ void d0q_wave(D0QScratch& sc, const Fe* __restrict__ X, uint64_t H, uint64_t nch,
+                                         uint64_t nk, uint64_t ch0, uint64_t nb, uint32_t w, uint32_t tb, uint32_t g) {
+  constexpr int NT = ROLE == 0 ? 21 : 18;
+  i32x16 acc[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0;
+  auto jk = [&](uint64_t k) {  // group g of chunk ch0 + k nb (chunk 0 for a block without chunks)
+    const uint64_t c = ch0 + k * nb;
+    return (c < nch ? c : 0) * 32 + g;
+  };
+  auto products = [&](uint32_t b) {  // of the image in buffer b
+    if constexpr (ROLE == 0) {
+      d0q_half<0>(sc.img[b][w], acc);
+      d0q_half<1>(sc.img[b][w], acc);
+    } else {
+      d0q_role1(sc.img[b], acc);
+    }
+  };
+  // the next chunk's loads are never conditional (past the last chunk a wave
+  // loads it again): conditional loads made the compiler drain every load
+  // before the products, so no load was in flight during them
+  // two chunks in flight: buffers A (even k) and B (odd k), the loop unrolled
+  // by two so that no register copy waits for a load; iterations past nk
+  // (at most one) only load and meet the barrier
+  Fe ca[2][2], cb[2][2];
+  const uint64_t k1 = nk > 1 ? 1 : 0;
+  d0q_load(X, jk(0), H, 2 * (int)w, ca[0]);
+  d0q_load(X, jk(0), H, 2 * (int)w + 1, ca[1]);
+  d0q_load(X, jk(k1), H, 2 * (int)w, cb[0]);
+  d0q_load(X, jk(k1), H, 2 * (int)w + 1, cb[1]);
+  auto step = [&](uint64_t k, Fe (&cur)[2][2]) {
+    const uint64_t kn = k + 2 < nk ? k + 2 : (nk > 0 ? nk - 1 : 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      Fe x[2] = {cur[i][0], cur[i][1]};
+      d0q_load(X, jk(kn), H, 2 * (int)w + i, cur[i]);
+      if (k < nk) d0q_put(sc.img[k & 1], 2 * (int)w + i, tb, g, x);
+    }
+    if (k >= 1 && k <= nk) products((uint32_t)((k - 1) & 1));
+    __syncthreads();  // image k complete; image k - 1 consumed
+  };
+  for (uint64_t k = 0; k <= nk; k += 2) {  // nk <= kD0QDrain (the host sizes the grid)
+    step(k, ca);
+    step(k + 1, cb);
+  }
+  d0q_drain<ROLE>(acc, sc.T, w);
 }
 
 template <class F>
@@ -956,51 +1104,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_d0q(const Fe* __restrict__ A,
   const uint64_t nch = H / 32, nb = gridDim.x >> 1, ch0 = blockIdx.x >> 1;
   const uint64_t nk = ch0 < nch ? (nch - 1 - ch0) / nb + 1 : 0;  // this block's chunks: ch0 + k nb
   __syncthreads();
-  if (w == 3) {  // producer: lane = (table, group)
-    const uint32_t tb = l >> 5, g = l & 31;
-    const Fe* __restrict__ X = tb ? (pp ? P : S) : (pp ? M : A);
-    // corner q = 8 u0 + (corner of variables 1-3). Pair q = corners q, 8 + q (X0, X1
-    // along variable 0) sits in cq[q]; once pair q of chunk k is converted its
-    // registers take pair q of chunk k + 1, so one chunk is always in flight
-    // (8 pairs, 128 VGPRs)
-    Fe cq[8][2];
-    auto load_pair = [&](uint64_t k, int q) {
-      const uint64_t j = (ch0 + k * nb) * 32 + g;
-      cq[q][0] = ld_fe(X, j + (uint64_t)q * H);
-      cq[q][1] = ld_fe(X, j + (uint64_t)(8 + q) * H);
-    };
-    if (nk > 0)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) load_pair(0, q);
-    for (uint64_t k = 0; k < nk; ++k) {
-      const uint32_t buf = (uint32_t)(k & 1);
-      const bool more = k + 1 < nk;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        Fe x0 = cq[q][0], x1 = cq[q][1];
-        if (more) load_pair(k + 1, q);
-        Fe d = sub256(x1, x0);  // X(inf) in (-p, p)
-        to_digits(d);
-        st_row(&sc.img[buf][2][q][tb][g][0], d);
-        to_digits(x0);
-        st_row(&sc.img[buf][0][q][tb][g][0], x0);
-        to_digits(x1);
-        st_row(&sc.img[buf][1][q][tb][g][0], x1);
-      }
-      __syncthreads();  // image k complete
-    }
-  } else {  // consumers: wave w multiplies point t0 = w
-    i32x16 acc[27];
-#pragma unroll
-    for (int i = 0; i < 27; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0;
-    for (uint64_t k = 0; k < nk; ++k) {  // nk <= kD0QDrain (the host sizes the grid)
-      __syncthreads();  // image k is complete
-      d0q_mfmas(sc.img[k & 1][w], acc);
-    }
-    d0q_drain(acc, sc.T, w);
-  }
+  const uint32_t tb = l >> 5, g = l & 31;
+  const Fe* __restrict__ X = tb ? (pp ? P : S) : (pp ? M : A);
+  if (w < 3)
+    d0q_wave<0>(sc, X, H, nch, nk, ch0, nb, w, tb, g);
+  else
+    d0q_wave<1>(sc, X, H, nch, nk, ch0, nb, w, tb, g);
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
   ZK_BLOCK_STAMP(sink, 0);
   __syncthreads();  // every drain is in T; the image is free for the epilogue
@@ -1024,6 +1133,17 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_d0q(const Fe* __restrict__ A,
 struct DM3Scratch : DMScratch {
   Fe eqw[8];
 };
+// 8 inputs of a fold (weights wf[0..7]) into its two MFMA accumulators
+__device__ __forceinline__ void fold_acc8(Fe (&x)[8], const i32x4* wf, i32x16& acc0, i32x16& acc1) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    to_digits(x[c]);
+    i32x4 b0, b1;
+    fold_operands(x[c], b0, b1);
+    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], b0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], b1, acc1, 0, 0, 0);
+  }
+}
 template <class F, int NP = 3>
 __device__ __forceinline__ Fe dm3_fold(Fe (&x)[1 << NP], const i32x4 (&wf)[1 << NP]) {
   i32x16 acc0, acc1;
@@ -1167,11 +1287,19 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   // Block 0's wave 0 polls the host for the challenges and relays them to
   // every block: its poll would wait behind these loads (vmcnt is in order),
   // so it loads after the challenges arrive.
-  Fe nx[NI], nx2[NP == 3 ? NI : 1];
+  // OCT 64 streams units of 8 inputs (a fold by three: one unit, by four: two;
+  // unit u = U f + h holds inputs 8 h .. 8 h + 7 of fold f), two units ahead
+  constexpr int U = NI / 8;
+  auto unit_at = [&](uint64_t ch, int u, Fe (&x)[8]) {
+    const uint64_t e = ch * 64 + l + (uint64_t)(u / U) * O + (uint64_t)(8 * (u % U)) * h8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
+  };
+  Fe nx[8], nx2[8];
   const bool early = OCT == 64 && (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
   if (early) {
-    in_at(blockIdx.x, 0, nx);
-    if constexpr (NP == 3) in_at(blockIdx.x, 1, nx2);
+    unit_at(blockIdx.x, 0, nx);
+    unit_at(blockIdx.x, 1, nx2);
   }
   // the third word group carries rc for this step; a fold by four reads a fourth group
   if constexpr (NP == 4)
@@ -1179,8 +1307,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   else
     block_get_rs(din, ra, rb, rc, gridDim.x > 1);
   if (OCT == 64 && !early && (uint64_t)blockIdx.x < nch) {
-    in_at(blockIdx.x, 0, nx);
-    if constexpr (NP == 3) in_at(blockIdx.x, 1, nx2);
+    unit_at(blockIdx.x, 0, nx);
+    unit_at(blockIdx.x, 1, nx2);
   }
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ T33Scratch sc;
@@ -1213,26 +1341,31 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
-      Fe x[NI];
-      if constexpr (NP == 4) {  // one fold ahead (16 inputs in flight)
+      i32x16 a0, a1;
 #pragma unroll
-        for (int k = 0; k < NI; ++k) x[k] = nx[k];
-        if (f < 7)
-          in_at(ch, f + 1, nx);
-        else if (ch + gridDim.x < nch)
-          in_at(ch + gridDim.x, 0, nx);
-      } else {
+      for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0;
 #pragma unroll
-        for (int k = 0; k < NI; ++k) {
+      for (int h = 0; h < U; ++h) {
+        Fe x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
           x[k] = nx[k];
           nx[k] = nx2[k];
         }
-        if (f < 6)
-          in_at(ch, f + 2, nx2);
-        else if (ch + gridDim.x < nch)
-          in_at(ch + gridDim.x, f - 6, nx2);
+        // the unit two ahead; past the block's last chunk its own chunk again
+        // (L2-hot): loads that are not conditional keep the compiler's vmcnt
+        // waits exact (a conditional load made it drain every load at each
+        // chunk boundary)
+        const int u2 = U * f + h + 2;
+        if (u2 < 8 * U)
+          unit_at(ch, u2, nx2);
+        else
+          unit_at(ch + gridDim.x < nch ? ch + gridDim.x : ch, u2 - 8 * U, nx2);
+        fold_acc8(x, &wf[8 * h], a0, a1);
       }
-      const Fe z = dm3_fold<F, NP>(x, wf);
+      int64_t W[8];
+      fold_words(a0, a1, W);
+      const Fe z = dm_finish<F>(W, fe_zero<F>());
       st_fold(X2, ch * 64 + l + (uint64_t)f * O, z);
       dm_row<F>(img[f][w][l], z);
     }
