@@ -625,12 +625,12 @@ def main() -> None:
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
 
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "r2_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r3_traffic.json")
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
         if t.get("kind") == dom and field == 0:  # the longest launch of this workload
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
-            traffic_src = f"profiles/r2_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
+            traffic_src = f"profiles/r3_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
     if rank == 0:
         out = {
