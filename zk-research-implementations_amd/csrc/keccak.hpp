@@ -26,7 +26,25 @@ struct Keccak256 {
 
   static inline uint64_t rol(uint64_t x, int s) { return (x << s) | (x >> (64 - s)); }
 
+  // The permutation body is compiled twice: with BMI1/BMI2 (andn for chi,
+  // rorx for the rotations) for hosts that have them, and for baseline
+  // x86-64; permute() picks one once per process. The transcript's absorb of
+  // a plain prove's table is a serial sponge on the host, so its
+  // speed is the floor of plain prove / verify.
   static void permute(uint64_t* A) {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+    static const bool bmi = __builtin_cpu_supports("bmi") && __builtin_cpu_supports("bmi2");
+    if (bmi) {
+      permute_bmi(A);
+      return;
+    }
+#endif
+    permute_body(A);
+  }
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+  __attribute__((target("bmi,bmi2"))) static void permute_bmi(uint64_t* A) { permute_body(A); }
+#endif
+  __attribute__((always_inline)) static inline void permute_body(uint64_t* A) {
     static const uint64_t RC[24] = {
         0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
         0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
