@@ -276,6 +276,29 @@ def test_three_round_first_pass_agrees_large(monkeypatch, field, n):
 
 
 @pytest.mark.parametrize("field", [0, 1, 2])
+@pytest.mark.parametrize("n", [15, 16, 17, 18, 19, 20])
+def test_four_round_first_pass_matches_oracle(monkeypatch, field, n):
+    """ZK_D0Q=1 (off by default, measured slower: DESIGN.md §3a''): rounds 0-3
+    in one pass over the inputs (k_gkr_d0q: 81 tiles, points 0, 1, inf along
+    variable 0 times the 27 moments of variables 1-3, products split over the
+    four waves), a fold by four challenges (k_gkr_t43, K = 512, inputs
+    streamed in units of eight) with rounds 4-6, then the triple steps as
+    after k_gkr_d0t. The oracle's proof, pre-enqueued or not, and with
+    ZK_GRID_CAP=2 (every block walks many chunks: the two-deep load ring of
+    k_gkr_d0q and its past-the-end clamp)."""
+    want = _oracle(field, n)
+    monkeypatch.setenv("ZK_D0Q", "1")
+    for pre, cap in (("1", "0"), ("0", "0"), ("1", "2")):
+        monkeypatch.setenv("ZK_PRELAUNCH", pre)
+        monkeypatch.setenv("ZK_GRID_CAP", cap)
+        ctx = zk_amd.Context(0)
+        try:
+            assert _prove(ctx, field, n) == want, f"ZK_PRELAUNCH={pre} ZK_GRID_CAP={cap}"
+        finally:
+            ctx.close()
+
+
+@pytest.mark.parametrize("field", [0, 1, 2])
 @pytest.mark.parametrize("n", [8, 10, 12, 15, 16, 19])
 def test_host_rounds_match_oracle(monkeypatch, field, n):
     """The last ZK_HOST_ROUNDS rounds on the host (host.hpp "host rounds"): the
