@@ -896,10 +896,6 @@ __device__ __forceinline__ void grid_finish_wide(Sc& sc, const RoundSink& sk) {
 // chunk, and a spill of an inline-asm MFMA's result would race the MFMA.
 template <int SLOT>
 __device__ __forceinline__ void d0q_mfma(i32x16& acc, const i32x4& a, const i32x4& b) {
-#if defined(ZK_D0Q_BUILTIN)
-  acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
-  return;
-#endif
   if constexpr (SLOT < 16)
     asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else
