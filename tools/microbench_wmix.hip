@@ -114,7 +114,11 @@ float run(const Tabs& t, size_t O, int grid, int reps) {
 
 // the real kernel's schedule: the next fold's NIN inputs are loaded (into registers)
 // before the current fold is combined and stored (one fold ahead); ST = store or not
-template <int NIN, int NF, bool ST>
+// LDC / STC: loads / stores lane-contiguous (instruction i of a wave moves the
+// i-th contiguous KiB of the wave's 2 KiB run: whole lines per instruction)
+// instead of the kernel's element-per-lane shape (lane l: bytes 32 l .. 32 l + 31
+// in two 16-B instructions, each touching every line of the run half)
+template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false>
 __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const uint4* __restrict__ X = t.in[w];
@@ -125,8 +129,14 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
     const size_t e = ch * 64 + l + (size_t)f * O;
 #pragma unroll
     for (int k = 0; k < NIN; ++k) {
-      na[k] = X[2 * (e + k * hs)];
-      nb[k] = X[2 * (e + k * hs) + 1];
+      if (LDC) {
+        const size_t r = ch * 64 + (size_t)f * O + k * hs;  // the run's first element
+        na[k] = X[2 * r + l];
+        nb[k] = X[2 * r + 64 + l];
+      } else {
+        na[k] = X[2 * (e + k * hs)];
+        nb[k] = X[2 * (e + k * hs) + 1];
+      }
     }
   };
   if (blockIdx.x < nch) load(blockIdx.x, 0);
@@ -148,7 +158,11 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
         xr(b, cb[k]);
       }
       const size_t e = ch * 64 + l + (size_t)f * O;
-      if (ST) {
+      if (ST && STC) {
+        const size_t r = ch * 64 + (size_t)f * O;
+        X2[2 * r + l] = a;
+        X2[2 * r + 64 + l] = b;
+      } else if (ST) {
         X2[2 * e] = a;
         X2[2 * e + 1] = b;
       } else if ((a.x ^ b.y) == 0x12345678u) {
@@ -158,7 +172,7 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
   }
 }
 
-template <int NIN, int NF, bool ST>
+template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false>
 float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   const size_t in_max = (O - 1) + (size_t)(NF - 1) * O + (size_t)(NIN - 1) * NF * O, out_max = NF * O - 1;
   if (O % 64 || in_max >= (1ull << 24) || out_max >= (1ull << 24) / 8) {
@@ -171,7 +185,7 @@ float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   std::vector<float> v;
   for (int r = 0; r < reps; ++r) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_mix_pf<NIN, NF, ST>), dim3(grid), dim3(256), 0, 0, t, O);
+    hipLaunchKernelGGL((k_mix_pf<NIN, NF, ST, LDC, STC>), dim3(grid), dim3(256), 0, 0, t, O);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -182,6 +196,14 @@ float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
   return v[v.size() / 2];
+}
+
+// plain copy of 2^24 x 32 B per table (read + write the same bytes), lane-contiguous uint4
+__global__ __launch_bounds__(256) void k_copy(Tabs t, size_t n4) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* __restrict__ X = t.in[w];
+  uint4* __restrict__ Y = t.out[w];
+  for (size_t i = (size_t)blockIdx.x * 64 + l; i < n4; i += (size_t)gridDim.x * 64) Y[i] = X[i];
 }
 
 int main() {
@@ -196,28 +218,39 @@ int main() {
   }
   const double rd = 4.0 * N * 32;
   const int reps = 7;
-  for (int grid : {256, 512, 1024}) {
-    const size_t O8 = N / 64, O16 = N / 256;  // fold by three writes 8 O8 = N/8, fold by four 16 O16 = N/16
-    float r8 = run<R8, 8, 8>(t, O8, grid, reps);
-    float w8 = run<W8, 8, 8>(t, O8, grid, reps);
-    float w8c = run<W8C, 8, 8>(t, O8, grid, reps);
-    float w8b = run<W8B, 8, 8>(t, O8, grid, reps);
-    float r16 = run<R16, 16, 16>(t, O16, grid, reps);
-    float w16 = run<W16, 16, 16>(t, O16, grid, reps);
-    const double wr8 = 4.0 * N / 8 * 32, wr16 = 4.0 * N / 16 * 32;
-    printf("grid %4d: R8 %6.1f us (%.2f TB/s) | W8 %6.1f (%.2f) | W8C %6.1f (%.2f) | W8B %6.1f (%.2f) | "
-           "R16 %6.1f (%.2f) | W16 %6.1f (%.2f)\n",
-           grid, r8, rd / r8 / 1e6, w8, (rd + wr8) / w8 / 1e6, w8c, (rd + wr8) / w8c / 1e6, w8b,
-           (rd + wr8) / w8b / 1e6, r16, rd / r16 / 1e6, w16, (rd + wr16) / w16 / 1e6);
-    fflush(stdout);
+  {  // calibration: copy 4 x 256 MiB (the output buffers hold N/8 elements: copy that much)
+    const size_t n4 = N / 8 * 2;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int grid : {1024, 4096}) {
+      std::vector<float> v;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_copy, dim3(grid), dim3(256), 0, 0, t, n4);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.push_back(ms * 1000.f);
+      }
+      std::sort(v.begin(), v.end());
+      printf("copy (4 x %zu MiB read + written), grid %d: %.1f us = %.2f TB/s (read + write)\n", n4 * 16 >> 20, grid,
+             v[reps / 2], 2.0 * 4 * n4 * 16 / v[reps / 2] / 1e6);
+    }
   }
   for (int grid : {256, 512}) {
-    const size_t O8 = N / 64, O16 = N / 256;
+    const size_t O8 = N / 64;
+    const double wr8 = 4.0 * N / 8 * 32;
     float r8 = run_pf<8, 8, false>(t, O8, grid, reps), w8 = run_pf<8, 8, true>(t, O8, grid, reps);
-    float r16 = run_pf<16, 16, false>(t, O16, grid, reps), w16 = run_pf<16, 16, true>(t, O16, grid, reps);
-    const double wr8 = 4.0 * N / 8 * 32, wr16 = 4.0 * N / 16 * 32;
-    printf("prefetch one fold ahead, grid %4d: R8 %6.1f us (%.2f TB/s) | W8 %6.1f (%.2f) | R16 %6.1f (%.2f) | W16 %6.1f (%.2f)\n",
-           grid, r8, rd / r8 / 1e6, w8, (rd + wr8) / w8 / 1e6, r16, rd / r16 / 1e6, w16, (rd + wr16) / w16 / 1e6);
+    float r8l = run_pf<8, 8, false, true>(t, O8, grid, reps);
+    float w8ls = run_pf<8, 8, true, true, false>(t, O8, grid, reps);
+    float w8sl = run_pf<8, 8, true, false, true>(t, O8, grid, reps);
+    float w8ll = run_pf<8, 8, true, true, true>(t, O8, grid, reps);
+    printf("fold by three, one fold ahead, grid %4d: R8 %6.1f us (%.2f TB/s) | W8 %6.1f (%.2f) | R8 lane-contig loads %6.1f (%.2f) | "
+           "W8 lc loads %6.1f (%.2f) | W8 lc stores %6.1f (%.2f) | W8 lc both %6.1f (%.2f)\n",
+           grid, r8, rd / r8 / 1e6, w8, (rd + wr8) / w8 / 1e6, r8l, rd / r8l / 1e6, w8ls, (rd + wr8) / w8ls / 1e6, w8sl,
+           (rd + wr8) / w8sl / 1e6, w8ll, (rd + wr8) / w8ll / 1e6);
     fflush(stdout);
   }
   return 0;
