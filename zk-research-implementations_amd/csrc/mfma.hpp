@@ -1276,15 +1276,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
 #pragma unroll
     for (int k = 0; k < NI; ++k) x[k] = ld_fe(X, e + k * h8);
   };
-  // inputs two folds ahead (one wave per SIMD: the loads in flight are what
-  // hides HBM latency). OCT 64: the first two folds' inputs (written by the
-  // previous kernel) are in flight while the host posts the challenges (OCT
-  // 32 loads them after the constants: held across them it spills)
+  // Inputs two units of eight ahead (one wave per SIMD: the loads in flight
+  // are what hides HBM latency); OCT 64 streams units (a fold by three: one
+  // unit per fold, by four: two; unit u = U f + h holds inputs 8 h .. 8 h + 7
+  // of fold f), OCT 32 whole folds. OCT 64: the first two units (written by
+  // the previous kernel) are in flight while the host posts the challenges
+  // (OCT 32 loads them after the constants: held across them it spills).
   // Block 0's wave 0 polls the host for the challenges and relays them to
   // every block: its poll would wait behind these loads (vmcnt is in order),
   // so it loads after the challenges arrive.
-  // OCT 64 streams units of 8 inputs (a fold by three: one unit, by four: two;
-  // unit u = U f + h holds inputs 8 h .. 8 h + 7 of fold f), two units ahead
   constexpr int U = NI / 8;
   auto unit_at = [&](uint64_t ch, int u, Fe (&x)[8]) {
     const uint64_t e = ch * 64 + l + (uint64_t)(u / U) * O + (uint64_t)(8 * (u % U)) * h8;
