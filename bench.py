@@ -89,6 +89,21 @@ def proof_check(field: int, n: int, seed: int, coeffs, nco, ch) -> dict:
     return out
 
 
+def kzg_commit_check(nvars: int, out) -> dict:
+    """The config-5 commitment (affine x, y limbs) against the committed fixture
+    f(taus) * G1 (tests/golden/kzg.json, from the C oracle's MLE evaluation and
+    kzg_oracle.mul via tests/golden/make_kzg_golden.py). A mismatch aborts the
+    bench, as for the proof digest."""
+    x = sum(int(out[0, i]) << (64 * i) for i in range(6))
+    y = sum(int(out[0, 6 + i]) << (64 * i) for i in range(6))
+    key = f"bls12_381_fr_{nvars}_s5"
+    path = os.path.join(ROOT, "tests", "golden", "kzg.json")
+    fix = json.load(open(path)).get(key) if os.path.exists(path) else None
+    if fix and (x, y) != (int(fix["commit_x"], 16), int(fix["commit_y"], 16)):
+        raise SystemExit(f"KZG commitment ({x:#x}, {y:#x}) != oracle fixture ({key})")
+    return {"fixture": f"tests/golden/kzg.json[{key}]" if fix else None, "matches_oracle_fixture": bool(fix) or None}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -415,6 +430,7 @@ def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
         ts.append(time.perf_counter() - t0)
     commit_ms = sorted(ts)[reps // 2] * 1e3
     k.close()
+    commit_check = kzg_commit_check(nvars, out)
     n = 1 << nvars
     return {
         "workload": f"BLS12-381: gkr_prove over {nvars} variables (A*S + M*P, seed 5) and the KZG commitment of a "
@@ -424,6 +440,7 @@ def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
         "kzg_setup_ms": setup_ms,
         "kzg_commit_ms": commit_ms,
         "msm_points_per_s": n / (commit_ms / 1e3),
+        "commit_check": commit_check,
         "note": "the reference commits with a naive sum of 2^24 full scalar multiplications (kzg.rs:131-144)",
     }
 
@@ -567,17 +584,33 @@ def main() -> None:
             # during the LAST timed step only: their marker packets cost the GPU
             # ~5 us per round, so timing every step would inflate ms_per_step
             st0 = ctx.stats()
-            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33"])
+            ctx.set_timing_kinds([] if args.no_events else ["gkr_round0", "gkr_round", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33", "coll"])
         step()
     torch.cuda.synchronize()
+    local_s = time.perf_counter() - t0  # this rank's own time, before the closing barrier
     barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     st = ctx.stats()
+    launches = ctx.launches()
+    ranks = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # per rank (SCALE attribution): its own time before the closing barrier,
+        # the host's wait for round results, the collectives (count, and the
+        # time of the last timed proof's: RCCL events on the stream or the host
+        # communicator's callback wall time)
+        coll_ms = sum(x["ms"] for x in launches if x["kind"] == "coll")
+        mine = {"rank": rank, "own_ms_per_step": local_s * 1e3 / args.steps,
+                "host_wait_ms_per_step": st["host_wait_us"] / 1e3 / args.steps,
+                "host_work_ms_per_step": st["host_work_us"] / 1e3 / args.steps,
+                "collectives_per_step": st["collectives"] / args.steps,
+                "collective_ms_last_step": coll_ms,
+                "collective_launches_last_step": sum(1 for x in launches if x["kind"] == "coll")}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
     assert np.array_equal(first_challenges, ch), "proof changed between steps"
 
     ops = 32.0 * ((1 << n) - 1) * args.steps
@@ -613,15 +646,16 @@ def main() -> None:
                               "alg_GB": d["alg_bytes"] / 1e9,
                               "achieved_GBs": d["alg_bytes"] / (d["ms"] / 1e3) / 1e9 if d["ms"] else None}
     # the dominant kernel: the longest launch of the timed proof (k_gkr_t33 over
-    # the input tables at n = 24: rounds 3-5)
-    launches = ctx.launches()
+    # the input tables at n = 24: rounds 3-5); collectives are listed apart
+    colls = [x for x in launches if x["kind"] == "coll"]
+    launches = [x for x in launches if x["kind"] != "coll"]
     # --no-events: no launch was timed; the roofline fields then read 0
     top = max(launches, key=lambda x: x["ms"]) if launches else {"kind": "none", "ms": 0.0, "alg_bytes": 0.0}
     dom = top["kind"]
     all_b = sum(kind(nm)["alg_bytes"] for nm in per_kind)
     all_ms = sum(kind(nm)["ms"] for nm in per_kind)
     achieved = top["alg_bytes"] / (top["ms"] / 1e3) / 1e9 if top["ms"] else 0.0
-    kernel_ms = sum(v["ms"] for v in k.values())  # the timed (last) step
+    kernel_ms = sum(v["ms"] for kk, v in k.items() if kk != "coll")  # the timed (last) step
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
 
     traffic, traffic_src = None, None
@@ -689,6 +723,18 @@ def main() -> None:
                 "launches_by_kind": {kk: v["launches"] / args.steps for kk, v in k.items() if v["launches"]},
             },
         }
+        if ranks is not None:
+            own = [r["own_ms_per_step"] for r in ranks]
+            out["multi_rank"] = {
+                "note": "per rank over the timed steps; own_ms = a rank's time before the closing barrier, skew = "
+                        "max - min of it; collective_ms = the collectives of the last timed proof (RCCL: HIP events "
+                        "around each ncclAllReduce / ncclAllGather on the proof's stream; host communicator: the "
+                        "callback's wall time)",
+                "barrier_skew_ms_per_step": max(own) - min(own),
+                "collective_ms_per_proof_max": max(r["collective_ms_last_step"] for r in ranks),
+                "collective_us_each_rank0": [round(x["ms"] * 1e3, 2) for x in colls],
+                "ranks": ranks,
+            }
         if cfg4 is not None:
             out["config4_26var"] = cfg4
         if not args.no_e2e and world == 1:

@@ -81,10 +81,12 @@ enum {
   ZK_K_GKR_TAIL = 10,  /* the small rounds of a proof in one persistent kernel (k_gkr_tail, ZK_DROUND=0) */
   ZK_K_GKR_DROUND = 11, /* two rounds per kernel: pending folds + round sums + next round's quadratics (k_gkr_dround) */
   ZK_K_GKR_DTAIL = 12, /* the small double rounds in one persistent kernel (k_gkr_dtail) */
-  ZK_K_GKR_D0 = 13,    /* rounds 0 and 1 in one pass over the input tables (k_gkr_d0m on the matrix cores; k_gkr_d0r / k_gkr_d0) */
+  ZK_K_GKR_D0 = 13,    /* the input pass: rounds 0-2 (k_gkr_d0t) or rounds 0 and 1 (k_gkr_d0m), on the matrix cores */
   ZK_K_GKR_DM = 14,    /* two-round steps on the matrix cores that fold by two or three challenges (k_gkr_dm, k_gkr_dm3) */
   ZK_K_GKR_T33 = 15,   /* three-round steps on the matrix cores: fold by three + 27 moment sums (k_gkr_t33) */
-  ZK_K_KINDS = 16
+  ZK_K_COLL = 16,      /* collectives of a sharded proof: RCCL all-reduce / all-gather (event-timed on the stream
+                          when timing is on), or the host communicator's callback (host wall time, always) */
+  ZK_K_KINDS = 17
 };
 typedef struct {
   uint64_t launches[ZK_K_KINDS];
@@ -95,6 +97,7 @@ typedef struct {
   uint64_t collectives;          /* all-reduce calls */
   double host_wait_us;           /* host time spent waiting for round results */
   double host_work_us;           /* host time from a round result to the next launch issued */
+  uint64_t device_fs_rounds;     /* rounds whose challenge the device drew (ZK_DEVICE_FS), replayed by the host */
 } zk_stats;
 int zk_ctx_set_timing(zk_ctx* ctx, int enable);                /* all kinds on / off */
 int zk_ctx_set_timing_mask(zk_ctx* ctx, uint32_t kind_mask);   /* bit k = time ZK_K_k launches */
@@ -282,7 +285,13 @@ int zk_gkr_circuit_prove_kzg(zk_ctx* ctx, zk_repr repr, uint32_t nlayers, const 
                              zk_fe* out_coeffs, uint8_t* out_ncoeffs, zk_fe* out_challenges, zk_fe* out_claims,
                              zk_fe* out_input_evals, zk_g1* out_commitment, zk_g1* out_proofs, zk_g2* out_g2_taus);
 /* gkr::verify (:128-227) with the two KZG::verify checks of the input layer
- * (:155-175) at the verifier's own (r_b, r_c): needs no inputs. */
+ * (:155-175) at the verifier's own (r_b, r_c): needs no inputs.
+ * SOUNDNESS: g2_taus must come from a trusted setup the verifier holds, NOT
+ * from the proof. The reference passes the prover's kzg_setup.g2_taus
+ * (gkr_protocol.rs:167,175), and this entry point keeps that behaviour for
+ * parity. A prover who picks its own setup can satisfy both pairings, so
+ * this check is not sound against a malicious prover unless the caller
+ * supplies g2_taus of its own (zk_kzg_g2_taus of a setup it trusts). */
 int zk_gkr_circuit_verify_kzg(zk_repr repr, uint32_t nlayers, const uint32_t* gates, const uint8_t* ops,
                               const zk_fe* output_poly, const zk_fe* coeffs, const uint8_t* ncoeffs,
                               const zk_fe* claims, const zk_fe* opened_evals, const zk_g1* commitment,

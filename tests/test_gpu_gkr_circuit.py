@@ -22,9 +22,24 @@ def _circuit(rng: random.Random, depth: int, out_gates: int) -> list[list[str]]:
     return [[rng.choice((A, M)) for _ in range(out_gates << (depth - 1 - i))] for i in range(depth)]
 
 
+@pytest.mark.parametrize("host_lgl", ["8", "0", "3"])
 @pytest.mark.parametrize("field,depth,out_gates", [(2, 3, 1), (0, 3, 1), (1, 4, 2), (2, 5, 1), (0, 1, 1), (0, 1, 2),
                                                    (2, 2, 2), (0, 5, 2)])
-def test_device_proof_equals_oracle(ctx, field, depth, out_gates):
+def test_device_proof_equals_oracle(monkeypatch, field, depth, out_gates, host_lgl):
+    """ZK_CIRCUIT_HOST_LGL: layers with tables of <= 2^this entries run on the
+    host (8, the default: these circuits entirely), none (0: every layer on the
+    device), or the top ones (3). Every split gives the oracle's proof."""
+    import zk_amd
+
+    monkeypatch.setenv("ZK_CIRCUIT_HOST_LGL", host_lgl)
+    ctx = zk_amd.Context(0)
+    try:
+        _check_circuit(ctx, field, depth, out_gates)
+    finally:
+        ctx.close()
+
+
+def _check_circuit(ctx, field, depth, out_gates):
     rng = random.Random(1000 * field + 10 * depth + out_gates)
     structure = _circuit(rng, depth, out_gates)
     p = go.MODULI[field]
@@ -54,7 +69,9 @@ def test_reference_circuit(ctx):  # gkr_protocol.rs:473-506
 def test_two_phase_equals_dense_tables(monkeypatch, field):
     """The default layer prover (two phases over tables of L = 2G entries) and
     ZK_CIRCUIT_DENSE=1 (the four L^2 tables, then the generic sum-check) give
-    the same proof on a 2^10-input circuit (input layer: 20 sum-check rounds)."""
+    the same proof on a 2^10-input circuit (input layer: 20 sum-check rounds);
+    so do every layer on the device (ZK_CIRCUIT_HOST_LGL=0) and every layer on
+    the host (10)."""
     import zk_amd
 
     rng = random.Random(5 + field)
@@ -64,8 +81,9 @@ def test_two_phase_equals_dense_tables(monkeypatch, field):
     inputs = [rng.randrange(p) for _ in range(1 << depth)]
     circ = Circuit(structure, field)
     proofs = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("ZK_CIRCUIT_DENSE", mode)
+    for mode in ("0", "1", "host0", "host10"):
+        monkeypatch.setenv("ZK_CIRCUIT_DENSE", "1" if mode == "1" else "0")
+        monkeypatch.setenv("ZK_CIRCUIT_HOST_LGL", mode[4:] if mode.startswith("host") else "8")
         c = zk_amd.Context(0)
         try:
             pr = prove(circ, inputs, c)
@@ -73,7 +91,7 @@ def test_two_phase_equals_dense_tables(monkeypatch, field):
                             pr.input_evaluations, pr.output_poly)
         finally:
             c.close()
-    assert proofs["0"] == proofs["1"]
+    assert proofs["0"] == proofs["1"] == proofs["host0"] == proofs["host10"]
 
 
 @pytest.mark.parametrize("field", [0, 2])

@@ -163,3 +163,37 @@ def test_verify_random_12_var_opening(ctx):
     bad[5] = ko.add(bad[5], ko.G1)
     assert not KZG.verify(c, v, bad, point, g2t)
     k.close()
+
+
+@pytest.mark.parametrize("n", [22, 24])
+def test_full_size_commit_equals_mle_value_times_g(ctx, n):
+    """BASELINE config 5 at full size (kzg.rs:51-53,131-144): the commitment of
+    the bench's 2^n-point table through zk_dev_kzg_commit, whose window width
+    grows with n (kzg.hip msm_g1_device: c = 19 at 2^22 with 14 windows, 20
+    at 2^24 with 13 windows of 2^20 buckets — parameters the small tests never
+    reach), equals
+    f(taus) * G1 from the C oracle's MLE evaluation, and the committed fixture
+    (tests/golden/kzg.json, tests/golden/make_kzg_golden.py)."""
+    import json
+    import os
+
+    import coracle as co
+    import numpy as np
+
+    from zk_amd._lib import check, lib
+    from zk_amd.elems import ptr
+    from zk_amd.kzg import _points
+
+    rng = random.Random(55)  # bench.py config5 taus
+    taus = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    evals = ctx.synth(2, 1 << n, seed=5, table=0)
+    out = np.zeros((1, 12), np.uint64)
+    check(lib().zk_dev_kzg_commit(ctx.h, k.h, evals.ptr, ptr(out)))
+    got = _points(out)[0]
+    evals.free()
+    k.close()
+    v = co.evaluate(2, co.synth(2, 5, 0, 0, 1 << n), taus)
+    assert got == ko.mul(v, ko.G1)
+    fix = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kzg.json")))[f"bls12_381_fr_{n}_s5"]
+    assert got == (int(fix["commit_x"], 16), int(fix["commit_y"], 16))

@@ -111,21 +111,6 @@ def test_grid_capped_headline_matches_fixture(monkeypatch):
     assert blob_digest(0, polys, chal) == g["blob_keccak256"]
 
 
-@pytest.mark.parametrize("key", ["bn254_fr_24_s3", "bn254_fr_23_s3"])
-def test_four_round_first_pass_matches_fixture(monkeypatch, key):
-    """ZK_D0Q=1 at the headline size: k_gkr_d0q with 256 chunks per block and
-    k_gkr_t43 give the committed oracle proof (DESIGN.md §3a'')."""
-    g = LARGE[key]
-    monkeypatch.setenv("ZK_D0Q", "1")
-    c = zk_amd.Context(0)
-    try:
-        polys, chal = device_proof(c, g["field"], g["nvars"], g["seed"])
-    finally:
-        c.close()
-    assert chal == [h2i(x) for x in g["challenges"]]
-    assert blob_digest(g["field"], polys, chal) == g["blob_keccak256"]
-
-
 @pytest.mark.parametrize("n", [22, 24])
 def test_plain_prove_at_scale_vs_oracle(ctx, n):
     """Plain `prove` (sum_check_protocol.rs:25-52) at the bench sizes, bit for bit

@@ -301,7 +301,7 @@ def test_stats_and_timing(ctx):
     ctx.set_timing(False)
     st = ctx.stats()
     k = st["kernels"]
-    # rounds 0 and 1 in one pass over the inputs (k_gkr_d0r, ZK_D0 default), then
+    # rounds 0 and 1 in one pass over the inputs (k_gkr_d0m, ZK_D0 default), then
     # rounds (2,3) .. (10,11) two per step, each folding by two pending challenges
     # (the first straight from the inputs); these small steps run in one persistent
     # kernel (k_gkr_dtail), except the last ZK_HOST_ROUNDS (default 4) rounds:

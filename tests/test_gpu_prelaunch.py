@@ -6,8 +6,8 @@
 * From round 2 on two rounds run per kernel (k_gkr_dround, default); the
   proof is identical with one round per kernel (ZK_DROUND=0), for odd and
   even round counts, pre-enqueued or not. With ZK_D0=1 (default) even counts
-  run rounds 0 and 1 in one pass over the inputs (k_gkr_d0r; ZK_D0=2 the
-  8-lane k_gkr_d0); the proof is identical to ZK_D0=0 (round 0, then round 1).
+  below 11 (or ZK_D0T=0) run rounds 0 and 1 in one pass over the inputs
+  (k_gkr_d0m); the proof is identical to ZK_D0=0 (round 0, then round 1).
 * The small double steps run in one persistent kernel (k_gkr_dtail, default);
   the proof is identical with one launch per step (ZK_DTAIL=0), when it
   starts at the first double step over large tables (ZK_DTAIL_MAX_QUADS) and
@@ -126,12 +126,12 @@ def test_double_and_single_rounds_agree_20var(monkeypatch, field):
 @pytest.mark.parametrize("n", [2, 4, 8, 16])
 def test_first_double_step_matches_oracle(monkeypatch, field, n):
     """With ZK_D0=1 even variable counts start with rounds 0 and 1 in one pass
-    over the inputs (k_gkr_d0r: nine product sums, nothing written); ZK_D0=0
-    runs round 0 alone and round 1 as a single step. Both equal the oracle, pre-enqueued
-    and per-round launched."""
+    over the inputs (k_gkr_d0m: nine product sums on the matrix cores, nothing
+    written); ZK_D0=0 runs round 0 alone and round 1 as a single step. Both
+    equal the oracle, pre-enqueued and per-round launched."""
     want = _oracle(field, n)
-    monkeypatch.setenv("ZK_D0T", "0")  # the two-round first pass (even n >= 14 default to three rounds)
-    for d0 in ("3", "1", "2", "0"):  # 3: k_gkr_d0m (matrix cores), 1: k_gkr_d0r (3 lanes per quad-product), 2: k_gkr_d0 (8 lanes)
+    monkeypatch.setenv("ZK_D0T", "0")  # the two-round first pass (n >= 11 default to three rounds)
+    for d0 in ("1", "0"):
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_D0", d0)
             monkeypatch.setenv("ZK_PRELAUNCH", pre)
@@ -147,14 +147,14 @@ def test_first_double_step_agrees_22var(monkeypatch, field):
     n = 22
     got = {}
     monkeypatch.setenv("ZK_D0T", "0")
-    for d0 in ("3", "1", "2", "0"):
+    for d0 in ("1", "0"):
         monkeypatch.setenv("ZK_D0", d0)
         ctx = zk_amd.Context(0)
         try:
             got[d0] = _prove(ctx, field, n)
         finally:
             ctx.close()
-    assert got["3"] == got["1"] == got["0"] == got["2"]
+    assert got["1"] == got["0"]
 
 
 @pytest.mark.parametrize("field", [0, 2])
@@ -242,21 +242,16 @@ def test_three_round_first_pass_matches_oracle(monkeypatch, field, n):
     (k_gkr_d0t: 27 moment tiles of corner-pair products on the matrix cores);
     triple steps that fold by the three pending challenges (eq weights,
     K = 256) and sum three rounds as 27 moment tiles (k_gkr_t33); one
-    two-round step folding by three (k_gkr_dm3); double steps. ZK_TTAIL=1:
-    triple steps to the end with 0-2 two-round steps (k_gkr_dm3, k_gkr_dm) so
-    the rest is a multiple of three (n = 11..20 cover all three cases), the
-    small ones in the persistent k_gkr_ttail (pre-enqueued) or one k_gkr_ttail
-    launch per step (ZK_PRELAUNCH=0). ZK_D0T=0 keeps the two-round schedule.
-    All give the oracle's proof."""
+    two-round step folding by three (k_gkr_dm3); double steps. ZK_D0T=0 keeps
+    the two-round schedule. Both give the oracle's proof, pre-enqueued or not."""
     want = _oracle(field, n)
-    for d0t, tt in (("1", "0"), ("1", "1"), ("0", "0")):
+    for d0t in ("1", "0"):
         for pre in ("1", "0"):
             monkeypatch.setenv("ZK_D0T", d0t)
-            monkeypatch.setenv("ZK_TTAIL", tt)
             monkeypatch.setenv("ZK_PRELAUNCH", pre)
             ctx = zk_amd.Context(0)
             try:
-                assert _prove(ctx, field, n) == want, f"ZK_D0T={d0t} ZK_TTAIL={tt} ZK_PRELAUNCH={pre}"
+                assert _prove(ctx, field, n) == want, f"ZK_D0T={d0t} ZK_PRELAUNCH={pre}"
             finally:
                 ctx.close()
 
@@ -273,29 +268,6 @@ def test_three_round_first_pass_agrees_large(monkeypatch, field, n):
         finally:
             ctx.close()
     assert got["1"] == got["0"]
-
-
-@pytest.mark.parametrize("field", [0, 1, 2])
-@pytest.mark.parametrize("n", [15, 16, 17, 18, 19, 20])
-def test_four_round_first_pass_matches_oracle(monkeypatch, field, n):
-    """ZK_D0Q=1 (off by default, measured slower: DESIGN.md §3a''): rounds 0-3
-    in one pass over the inputs (k_gkr_d0q: 81 tiles, points 0, 1, inf along
-    variable 0 times the 27 moments of variables 1-3, products split over the
-    four waves), a fold by four challenges (k_gkr_t43, K = 512, inputs
-    streamed in units of eight) with rounds 4-6, then the triple steps as
-    after k_gkr_d0t. The oracle's proof, pre-enqueued or not, and with
-    ZK_GRID_CAP=2 (every block walks many chunks: the two-deep load ring of
-    k_gkr_d0q and its past-the-end clamp)."""
-    want = _oracle(field, n)
-    monkeypatch.setenv("ZK_D0Q", "1")
-    for pre, cap in (("1", "0"), ("0", "0"), ("1", "2")):
-        monkeypatch.setenv("ZK_PRELAUNCH", pre)
-        monkeypatch.setenv("ZK_GRID_CAP", cap)
-        ctx = zk_amd.Context(0)
-        try:
-            assert _prove(ctx, field, n) == want, f"ZK_PRELAUNCH={pre} ZK_GRID_CAP={cap}"
-        finally:
-            ctx.close()
 
 
 @pytest.mark.parametrize("field", [0, 1, 2])

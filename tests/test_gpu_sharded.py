@@ -169,25 +169,6 @@ def test_early_gather_matches_single_process(tmp_path, world, nloc, field, gathe
         assert r["collectives"] == _collectives(nloc, int(gather)), f"rank {rank}"
 
 
-@pytest.mark.parametrize("comm,world,nloc", [("host", 2, 18), ("rccl", 1, 18), ("host", 2, 21)])
-def test_four_round_first_pass_sharded(tmp_path, comm, world, nloc):
-    """ZK_D0Q=1 (off by default): the 729 limb sums of k_gkr_d0q go through
-    the wide all-reduce (RCCL, or the host communicator) and every rank gets
-    the single-process oracle's proof. Schedule per rank at nloc = 18 with
-    the default early gather (10): d0q (rounds 0-3), t43 (4-6), t33 (7-9),
-    then the gather: 4 collectives; at 21: d0q, t43, the two-round step that
-    folds by three (7-8), one double step (9-10) and the gather: 5."""
-    env = {"ZK_D0Q": "1"}
-    if comm == "rccl":
-        env["ZK_FORCE_COLLECTIVES"] = "1"
-    res = _run(world, comm, 0, nloc, str(tmp_path), env)
-    want = _oracle(0, nloc + world.bit_length() - 1)
-    for rank, r in enumerate(res):
-        assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
-        if comm == "host":
-            assert r["collectives"] == (4 if nloc == 18 else 5), f"rank {rank}"
-
-
 # G = 8, the world size of the 8-GPU node, on this one card: 8 worker
 # processes (host all-reduce over gloo; RCCL refuses ranks that share a
 # device). Exercises the 8-way low-bit shard layout, the [8][4][2^T] gather

@@ -2,7 +2,7 @@
 // check against the host permutation. hipcc -O3 --offload-arch=gfx950 tools/microbench_keccak.hip -o tools/mb_keccak
 #include <hip/hip_runtime.h>
 #include <stdio.h>
-#include "../zk-research-implementations_amd/csrc/dkeccak.hpp"
+#include "dkeccak.hpp"
 #include "../zk-research-implementations_amd/csrc/keccak.hpp"
 
 __global__ void k_keccak(uint64_t* st, int iters, unsigned long long* cycles) {

@@ -8,6 +8,7 @@
 //   W8B  : 8 inputs -> 1 output, the 8 outputs of a chunk stored together after its loads
 //   R16  : 16 inputs per output (fold by four), no stores
 //   W16  : 16 inputs -> 1 output (134 MB written)
+// and (round 4) R8 / W8 with the inputs landed in LDS by LDS-DMA (k_mix_glds).
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/mb_wmix tools/microbench_wmix.hip
 #include <hip/hip_runtime.h>
 
@@ -198,6 +199,95 @@ float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   return v[v.size() / 2];
 }
 
+// The same pattern with the inputs landed in LDS by LDS-DMA (global_load_lds_dwordx4:
+// no VGPR destination) instead of a register prefetch: each wave streams its own
+// table through a private ring of DEPTH units (a unit = KU of a fold's 8 inputs,
+// KU x 2 KiB), waits for a unit with a counted vmcnt (no barrier: every wave reads
+// only what it loaded itself), reads its element of each input (two ds_read_b128),
+// and stores the fold's output as the kernel does. WPS = waves per SIMD the launch
+// bound allows (LDS: 4 WPS waves x DEPTH x KU x 2 KiB per CU).
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int NF, bool ST, int KU, int DEPTH, int WPS>
+__global__ __launch_bounds__(256, WPS) void k_mix_glds(Tabs t, size_t O) {
+  constexpr int NIN = 8, UPF = NIN / KU;  // units per fold
+  __shared__ uint4 ring[4][DEPTH][KU][128];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* __restrict__ X = t.in[w];
+  uint4* __restrict__ X2 = t.out[w];
+  const size_t nch = O / 64, hs = (size_t)NF * O;
+  const size_t my = nch > blockIdx.x ? (nch - 1 - blockIdx.x) / gridDim.x + 1 : 0;  // chunks of this block
+  const size_t nu = my * NF * UPF;                                                  // units of this wave
+  auto issue = [&](size_t u) {  // unit u -> slot u % DEPTH (past the end: chunk 0 again, never read)
+    const size_t q = u < nu ? u : 0;
+    const size_t ch = blockIdx.x + (q / (NF * UPF)) * gridDim.x;
+    const int f = (int)((q / UPF) % NF), h = (int)(q % UPF);
+    const size_t e0 = ch * 64 + (size_t)f * O;
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+      const char* g = (const char*)(X + 2 * (e0 + (size_t)(h * KU + k) * hs)) + 16 * l;
+      __attribute__((address_space(3))) void* d = (__attribute__((address_space(3))) void*)&ring[w][u % DEPTH][k][0];
+      __builtin_amdgcn_global_load_lds((const void*)g, d, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(g + 1024), (__attribute__((address_space(3))) void*)&ring[w][u % DEPTH][k][64], 16, 0, 0);
+    }
+  };
+  if (nu == 0) return;
+#pragma unroll
+  for (int d = 0; d < DEPTH - 1; ++d) issue(d);
+  uint4 a = make_uint4(0, 0, 0, 0), b = a;
+  for (size_t u = 0; u < nu; ++u) {
+    issue(u + DEPTH - 1);
+    wait_vm<2 * KU * (DEPTH - 1)>();  // unit u landed (stores issued since count too: a conservative wait)
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+      xr(a, ring[w][u % DEPTH][k][2 * l]);
+      xr(b, ring[w][u % DEPTH][k][2 * l + 1]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads are done before it is refilled
+    if ((u + 1) % UPF == 0) {
+      const size_t q = u / UPF, ch = blockIdx.x + (q / NF) * gridDim.x;
+      const size_t e = ch * 64 + l + (q % NF) * O;
+      if (ST) {
+        X2[2 * e] = a;
+        X2[2 * e + 1] = b;
+      } else if ((a.x ^ b.y) == 0x12345678u) {
+        X2[2 * e] = a;
+      }
+      a = make_uint4(0, 0, 0, 0);
+      b = a;
+    }
+  }
+  wait_vm<0>();
+}
+
+template <int NF, bool ST, int KU, int DEPTH, int WPS>
+float run_glds(const Tabs& t, size_t O, int grid, int reps) {
+  const size_t in_max = (O - 1) + (size_t)(NF - 1) * O + (size_t)7 * NF * O, out_max = NF * O - 1;
+  if (O % 64 || in_max >= (1ull << 24) || out_max >= (1ull << 24) / 8) {
+    fprintf(stderr, "bad sizes: O %zu in_max %zu out_max %zu\n", O, in_max, out_max);
+    exit(1);
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> v;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_mix_glds<NF, ST, KU, DEPTH, WPS>), dim3(grid), dim3(256), 0, 0, t, O);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    v.push_back(ms * 1000.f);
+  }
+  std::sort(v.begin(), v.end());
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return v[v.size() / 2];
+}
+
 // plain copy of 2^24 x 32 B per table (read + write the same bytes), lane-contiguous uint4
 __global__ __launch_bounds__(256) void k_copy(Tabs t, size_t n4) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -251,6 +341,20 @@ int main() {
            "W8 lc loads %6.1f (%.2f) | W8 lc stores %6.1f (%.2f) | W8 lc both %6.1f (%.2f)\n",
            grid, r8, rd / r8 / 1e6, w8, (rd + wr8) / w8 / 1e6, r8l, rd / r8l / 1e6, w8ls, (rd + wr8) / w8ls / 1e6, w8sl,
            (rd + wr8) / w8sl / 1e6, w8ll, (rd + wr8) / w8ll / 1e6);
+    fflush(stdout);
+  }
+  // LDS-DMA landing (round 4): one wave per SIMD with whole folds in a 2-deep
+  // ring, and two waves per SIMD with half folds (4 inputs) in 2- and 3-deep rings
+  for (int grid : {256, 512, 1024}) {
+    const size_t O8 = N / 64;
+    const double wr8 = 4.0 * N / 8 * 32;
+    float r1 = run_glds<8, false, 8, 2, 1>(t, O8, grid, reps), w1 = run_glds<8, true, 8, 2, 1>(t, O8, grid, reps);
+    float r2 = run_glds<8, false, 4, 2, 2>(t, O8, grid, reps), w2 = run_glds<8, true, 4, 2, 2>(t, O8, grid, reps);
+    float w3 = run_glds<8, true, 2, 4, 2>(t, O8, grid, reps);
+    printf("LDS-DMA, grid %4d: 1 wave/SIMD (fold units, depth 2): R8 %6.1f us (%.2f TB/s) W8 %6.1f (%.2f) | 2 waves/SIMD "
+           "(half folds, depth 2): R8 %6.1f (%.2f) W8 %6.1f (%.2f) | 2 waves/SIMD (quarter folds, depth 4): W8 %6.1f (%.2f)\n",
+           grid, r1, rd / r1 / 1e6, w1, (rd + wr8) / w1 / 1e6, r2, rd / r2 / 1e6, w2, (rd + wr8) / w2 / 1e6, w3,
+           (rd + wr8) / w3 / 1e6);
     fflush(stdout);
   }
   return 0;

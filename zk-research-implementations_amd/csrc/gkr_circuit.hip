@@ -70,7 +70,7 @@ void gkr_layer_two_phase(zk_ctx* c, const Fe* w, const Fe* wt, const uint8_t* op
   out.coeffs.assign(3 * (size_t)nv, zk::fe_zero<F>());
   out.ncoeffs.assign(nv, 0);
   out.challenges.assign(nv, zk::fe_zero<F>());
-  ensure_partials(c);
+  ensure_partials(c, lgL);
   __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
   c->work[0].ensure(4 * std::max<uint64_t>(L / 2, 1) * 32);
   c->work[1].ensure(4 * std::max<uint64_t>(L / 4, 1) * 32);
@@ -95,6 +95,95 @@ void gkr_layer_two_phase(zk_ctx* c, const Fe* w, const Fe* wt, const uint8_t* op
   const Fe* cur2[4] = {t2, t2 + L, t2 + 2 * L, t2 + 3 * L};
   gkr_phase<F>(c, cur2, lgL, lgL, false, tr, out, claim, r, pend);  // rounds lgL .. 2 lgL-1 (c)
   sync(c);
+}
+
+// A small layer's sum-check entirely on the host (ZK_CIRCUIT_HOST_LGL): the
+// same two phases over the same four tables of L entries as
+// gkr_layer_two_phase, the same field values and transcript, with no device
+// round trip — on tables of a few hundred entries one host pass per round
+// takes microseconds, while each device step waits for a host hand-off. The
+// reference's own arithmetic: gkr_prove (sum_check_protocol.rs:86-115) with
+// get_round_partial_polynomial_proof_gkr (:152-166) and partial_evaluate
+// (multilinear_polynomial_evaluation.rs:52-63); each round's three values are
+// summed unreduced and reduced once.
+template <class F>
+void host_layer_phase(std::vector<Fe> (&T)[4], uint32_t n, uint32_t k0, zk_transcript* tr, GkrOut& out) {
+  using namespace zk;
+  Fe r;
+  for (uint32_t i = 0; i < n; ++i) {
+    const size_t h = T[0].size() / 2;
+    uint64_t a0[9] = {0}, a1[9] = {0}, a2[9] = {0};
+    for (size_t j = 0; j < h; ++j) {
+      h64::V x2[4];
+      for (int t = 0; t < 4; ++t) x2[t] = h64::of(hfe_sub<F>(hfe_add<F>(T[t][j + h], T[t][j + h]), T[t][j]));
+      h64::mac_wide(a0, h64::of(T[0][j]), h64::of(T[1][j]));
+      h64::mac_wide(a0, h64::of(T[2][j]), h64::of(T[3][j]));
+      h64::mac_wide(a1, h64::of(T[0][j + h]), h64::of(T[1][j + h]));
+      h64::mac_wide(a1, h64::of(T[2][j + h]), h64::of(T[3][j + h]));
+      h64::mac_wide(a2, x2[0], x2[1]);
+      h64::mac_wide(a2, x2[2], x2[3]);
+    }
+    finish_round<F>(tr, wide_to_fe<F>(a0), wide_to_fe<F>(a1), wide_to_fe<F>(a2), k0 + i, out, r);
+    if (i + 1 < n) host_fold<F>(T, r);
+  }
+}
+template <class F>
+Fe host_mle_eval(const Fe* w, uint32_t n, const Fe* pt) {  // MultilinearPoly::evaluate (:79-91)
+  std::vector<Fe> t(w, w + ((size_t)1 << n));
+  for (uint32_t k = 0; k < n; ++k) {
+    const size_t h = t.size() / 2;
+    for (size_t j = 0; j < h; ++j) t[j] = zk::hfe_add<F>(t[j], zk::hfe_mul<F>(pt[k], zk::hfe_sub<F>(t[j + h], t[j])));
+    t.resize(h);
+  }
+  return t[0];
+}
+// eq(pt, v) over n bits, MSB first
+template <class F>
+Fe host_eq(const Fe* pt, uint64_t v, uint32_t n) {
+  Fe e = zk::fe_one<F>();
+  for (uint32_t k = 0; k < n; ++k)
+    e = zk::hfe_mul<F>(e, ((v >> (n - 1 - k)) & 1u) ? pt[k] : zk::hfe_sub<F>(zk::fe_one<F>(), pt[k]));
+  return e;
+}
+// w = the layer's L inputs, wt = its G gate weights (k_gate_weights), ops its gate ops
+template <class F>
+void host_layer(const Fe* w, const std::vector<Fe>& wt, const uint8_t* ops, uint32_t lgL, zk_transcript* tr,
+                GkrOut& out) {
+  using namespace zk;
+  const uint32_t nv = 2 * lgL;
+  const size_t L = (size_t)1 << lgL;
+  out.coeffs.assign(3 * (size_t)nv, fe_zero<F>());
+  out.ncoeffs.assign(nv, 0);
+  out.challenges.assign(nv, fe_zero<F>());
+  std::vector<Fe> T[4];  // phase 1 (kernels.hpp k_phase1_tables): W = w, U, V, 1
+  for (auto& t : T) t.assign(L, fe_zero<F>());
+  for (size_t b = 0; b < L; ++b) {
+    T[0][b] = w[b];
+    T[3][b] = fe_one<F>();
+    if ((b & 1) == 0) {
+      const Fe x = wt[b >> 1], xw = hfe_mul<F>(x, w[b + 1]);
+      if (ops[b >> 1]) {
+        T[1][b] = xw;
+      } else {
+        T[1][b] = x;
+        T[2][b] = xw;
+      }
+    }
+  }
+  host_layer_phase<F>(T, lgL, 0, tr, out);
+  const Fe* rb = out.challenges.data();
+  const Fe wrb = host_mle_eval<F>(w, lgL, rb);
+  for (auto& t : T) t.assign(L, fe_zero<F>());  // phase 2 (k_phase2_tables): A, S, M, P over c
+  for (size_t cc = 0; cc < L; ++cc) {
+    if (cc & 1) {
+      const size_t b = cc - 1;
+      const Fe e = hfe_mul<F>(wt[b >> 1], host_eq<F>(rb, b, lgL));
+      (ops[b >> 1] ? T[2] : T[0])[cc] = e;
+    }
+    T[1][cc] = hfe_add<F>(wrb, w[cc]);
+    T[3][cc] = hfe_mul<F>(wrb, w[cc]);
+  }
+  host_layer_phase<F>(T, lgL, lgL, tr, out);
 }
 
 template <class F>
@@ -141,6 +230,21 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
   o.sc.ncoeffs.assign(total, 0);
   o.sc.challenges.assign(total, fe_zero<F>());
   uint32_t k0 = 0;
+  // layers with tables of <= 2^host_lgl entries run on the host (host_layer); their
+  // inputs (the top of vals) come over in one copy
+  const uint32_t host_lgl = c->circuit_host_lgl;
+  std::vector<Fe> hvals;
+  size_t hbase = nvals;
+  for (uint32_t l = 0; l < nlayers; ++l)
+    if (lg2u(2 * (uint64_t)gates[l]) <= host_lgl) {
+      hbase = off[l];
+      break;
+    }
+  if (hbase < nvals) {
+    hvals.resize(nvals - hbase);
+    HIPCK(hipMemcpyAsync(hvals.data(), vals.b.fe(hbase), hvals.size() * 32, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+  }
   static const bool dbg = getenv("ZK_DEBUG_CIRCUIT") != nullptr;
   using clk = std::chrono::steady_clock;
   auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -172,12 +276,30 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
       b = beta;
       has_c = 1;
     }
+    GkrOut g;
+    const bool on_host = lgL <= host_lgl && off[l] >= hbase;
+    Fe o1, o2;
+    if (on_host) {  // gate weights, both phases and both evaluations on the host
+      if (dbg) t1 = clk::now();
+      std::vector<Fe> wt(G);
+      for (uint32_t gi = 0; gi < G; ++gi) {  // k_gate_weights
+        Fe wg = hfe_mul<F>(a, host_eq<F>(pts.data(), gi, W));
+        if (has_c) wg = hfe_add<F>(wg, hfe_mul<F>(b, host_eq<F>(pts.data() + W, gi, W)));
+        wt[gi] = wg;
+      }
+      const Fe* hw = hvals.data() + (off[l] - hbase);
+      host_layer<F>(hw, wt, ops + opoff[l], lgL, &tr, g);
+      if (dbg) t2 = clk::now();
+      o1 = host_mle_eval<F>(hw, lgL, g.challenges.data());
+      o2 = host_mle_eval<F>(hw, lgL, g.challenges.data() + lgL);
+    }
     LayerPts lp{};
     std::copy(pts.begin(), pts.end(), lp.r);
-    launch(c, ZK_K_LAYER, 32.0 * G, (double)G * (W + 2), k_gate_weights<F>, (G + kBlock - 1) / kBlock, lp, W, a, b,
-           has_c, G, dwt.b.fe(0));
-    GkrOut g;
-    if (c->circuit_dense) {  // ZK_CIRCUIT_DENSE=1: the four L^2 tables, then the generic sum-check
+    if (!on_host)
+      launch(c, ZK_K_LAYER, 32.0 * G, (double)G * (W + 2), k_gate_weights<F>, (G + kBlock - 1) / kBlock, lp, W, a, b,
+             has_c, G, dwt.b.fe(0));
+    if (on_host) {
+    } else if (c->circuit_dense) {  // ZK_CIRCUIT_DENSE=1: the four L^2 tables, then the generic sum-check
       c->input.ensure(4 * T * 32);
       Fe* tab = c->input.fe();
       const uint32_t grid = grid_for(c, T, k_layer_tables<F>);
@@ -202,16 +324,18 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     k0 += nv;
     rb.assign(g.challenges.begin(), g.challenges.begin() + nv / 2);  // (:71-73)
     rc.assign(g.challenges.begin() + nv / 2, g.challenges.end());
-    // o1 = w.evaluate(r_b), o2 = w.evaluate(r_c) (:75-76): one fused pass
-    LayerPts ep{};
-    std::copy(rb.begin(), rb.end(), ep.r);
-    std::copy(rc.begin(), rc.end(), ep.r + lgL);
-    const zk::RoundSink sk = make_sink(c, false);
-    launch(c, ZK_K_LAYER, 32.0 * (2 * G), 4.0 * (2 * G), k_mle_eval2<F>, grid_for(c, 2 * (uint64_t)G, k_mle_eval2<F>), w,
-           lgL, ep, sk);
-    Fe ev[2];
-    collect_sums<F, 2>(c, sk, false, 17, ev);
-    const Fe o1 = ev[0], o2 = ev[1];
+    if (!on_host) {  // o1 = w.evaluate(r_b), o2 = w.evaluate(r_c) (:75-76): one fused pass
+      LayerPts ep{};
+      std::copy(rb.begin(), rb.end(), ep.r);
+      std::copy(rc.begin(), rc.end(), ep.r + lgL);
+      const zk::RoundSink sk = make_sink(c, false);
+      launch(c, ZK_K_LAYER, 32.0 * (2 * G), 4.0 * (2 * G), k_mle_eval2<F>, grid_for(c, 2 * (uint64_t)G, k_mle_eval2<F>),
+             w, lgL, ep, sk);
+      Fe ev[2];
+      collect_sums<F, 2>(c, sk, false, 17, ev);
+      o1 = ev[0];
+      o2 = ev[1];
+    }
     if (dbg)
       fprintf(stderr, "[circuit] layer %u nv %u: tables %.1f us, sum-check %.1f us (%.1f/round), evals %.1f us\n", idx,
               nv, us(t0, t1), us(t1, t2), us(t1, t2) / nv, us(t2, clk::now()));

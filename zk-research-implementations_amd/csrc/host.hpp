@@ -206,12 +206,8 @@ struct zk_ctx {
   bool prelaunch = true;    // pre-enqueue round kernels (ZK_PRELAUNCH=0 launches each after its challenge)
   bool host_prelaunch = false;  // ... also under a host communicator (ZK_HOST_PRELAUNCH; ranks on distinct devices only)
   bool dround = true;       // two rounds per kernel from round 2 on (ZK_DROUND=0: one round per kernel)
-  int d0 = 3;              // (dround, even variable count) rounds 0 and 1 from the inputs in one kernel (ZK_D0): 3 k_gkr_d0m (matrix cores), 1 k_gkr_d0r, 2 k_gkr_d0, 0 off
+  int d0 = 3;              // (dround, even variable count below 11 or ZK_D0T=0) rounds 0 and 1 from the inputs in one kernel, k_gkr_d0m (ZK_D0; 0 off)
   bool d0t = true;          // nv >= 11: rounds 0-2 in one pass, then steps that fold by three (ZK_D0T)
-  bool d0q = false;         // (d0t) rounds 0-3 in one pass, then one step that folds by four (ZK_D0Q; k_gkr_d0q, k_gkr_t33<.., 4>)
-  DevBuf wide;              // ZK_D0Q: [768 u64 limb accumulator][768 u64 all-reduce buffer] of the 729-limb step
-  uint64_t* h_wide = nullptr;  // pinned, device-mapped: its 729 round totals
-  bool ttail = false;       // (d0t) triple steps to the end, the small ones in k_gkr_ttail (ZK_TTAIL; slower)
   bool dm = true;           // double steps with two pending challenges on the matrix cores (k_gkr_dm; ZK_DM=0: k_gkr_dround)
   uint64_t dm_min_quads = 1u << 17;  // ... when they have at least this many quads (ZK_DM_MIN_QUADS; smaller steps are latency-bound: k_gkr_dround)
   bool dtail = true;        // the small double rounds in one persistent kernel (ZK_DTAIL=0: one launch each)
@@ -222,9 +218,12 @@ struct zk_ctx {
   uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
+  bool device_fs = false;    // the persistent tail draws its own challenges (ZK_DEVICE_FS; dfs.hpp)
+  zk::FsLog* h_fslog = nullptr;  // pinned, device-mapped: 64 records of device-drawn rounds
   size_t h_tab_bytes = 0;
   bool tail = true;         // (ZK_DROUND=0 only) pre-enqueued small rounds in one persistent kernel (ZK_TAIL=0: one launch each)
   bool circuit_dense = false;  // circuit GKR: dense L^2 layer tables instead of the two-phase prover (ZK_CIRCUIT_DENSE)
+  uint32_t circuit_host_lgl = 8;  // circuit GKR: layers with tables of <= 2^this entries run on the host (ZK_CIRCUIT_HOST_LGL)
   uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
   uint64_t* tail_trace = nullptr;      // ZK_DEBUG_TAIL: pinned per-round stamps of the tail kernel, printed per proof
   uint64_t* block_trace = nullptr;     // ZK_DEBUG_BLOCKS=<step>: pinned per-block stamps of that step (needs ZK_DEBUG_TAIL)
@@ -292,10 +291,14 @@ uint32_t grid_for(zk_ctx* c, uint64_t work, K kernel) {
 // by ZK_GRID_CAP (tests: several chunks per block at oracle-checkable sizes),
 // but never below `min_blocks`, the count that keeps every block within its
 // int32 tile bound (k*ChunksMax in mfma.hpp).
+// The grid must fit the partial-sum buffer (ensure_partials): checked here,
+// before anything is launched with it.
 inline uint32_t step_grid(zk_ctx* c, uint32_t res, uint64_t min_blocks) {
   uint64_t g = res;
   if (c->grid_cap > 0 && g > c->grid_cap) g = c->grid_cap;
-  return (uint32_t)std::max<uint64_t>({g, min_blocks, 1});
+  g = std::max<uint64_t>({g, min_blocks, 1});
+  if ((g + 8) * zk::kSlotU64 * 8 > c->partials.bytes) fail(ZK_EINVAL, "internal: step grid exceeds the partial-sum buffer");
+  return (uint32_t)g;
 }
 
 // Launch wrapper: counts algorithmic bytes / multiplications per kernel kind
@@ -366,16 +369,59 @@ Fe from_limb_sums(const uint64_t* w) {
 // ---------------------------------------------------------------------------
 inline bool multi_rank(zk_ctx* c) { return (c->world > 1 || c->force_coll) && c->comm != COMM_NONE; }
 
+// Collective timing (ZK_K_COLL): an RCCL collective on the stream is bracketed
+// by events when that kind is timed (its duration then joins the launch log
+// like a kernel's); a host communicator's callback is host wall time, counted
+// always. `bytes` = what this rank sends.
+struct CollTimer {
+  zk_ctx* c;
+  double bytes;
+  zk_ctx::Pending p{ZK_K_COLL, nullptr, nullptr, 0.0};
+  std::chrono::steady_clock::time_point t0;
+  CollTimer(zk_ctx* cc, double b) : c(cc), bytes(b) {
+    p.bytes = b;
+    if (c->comm == COMM_RCCL && ((c->timing >> ZK_K_COLL) & 1u)) {
+      if (c->ev_free.empty()) {
+        hipEvent_t a, e;
+        HIPCK(hipEventCreate(&a));
+        HIPCK(hipEventCreate(&e));
+        c->ev_free.push_back({a, e});
+      }
+      p.a = c->ev_free.back().first;
+      p.b = c->ev_free.back().second;
+      c->ev_free.pop_back();
+      HIPCK(hipEventRecord(p.a, c->stream));
+    }
+    t0 = std::chrono::steady_clock::now();
+  }
+  ~CollTimer() {
+    if (p.a) {
+      (void)hipEventRecord(p.b, c->stream);
+      c->pending.push_back(p);
+    } else if (c->comm == COMM_HOST) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      c->stats.kernel_ms[ZK_K_COLL] += ms;
+      if (c->launch_log.size() < kLaunchLogMax) c->launch_log.push_back(zk_launch{ZK_K_COLL, ms, bytes});
+    }
+    c->stats.launches[ZK_K_COLL] += 1;
+    c->stats.alg_bytes[ZK_K_COLL] += bytes;
+  }
+};
+
 // In-place SUM of n u64 over all ranks (host memory in/out). RCCL runs on the
 // ctx stream through a device bounce buffer; a host communicator runs its callback.
 inline void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
   if (c->comm == COMM_RCCL) {
     uint64_t* d = reinterpret_cast<uint64_t*>(d_gather(c));
     HIPCK(hipMemcpyAsync(d, w, n * 8, hipMemcpyHostToDevice, c->stream));
-    NCCLCK(ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, c->stream));
+    {
+      CollTimer ct(c, 8.0 * n);
+      NCCLCK(ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, c->stream));
+    }
     HIPCK(hipMemcpyAsync(w, d, n * 8, hipMemcpyDeviceToHost, c->stream));
     sync(c);
   } else if (c->comm == COMM_HOST) {
+    CollTimer ct(c, 8.0 * n);
     if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
   } else {
     fail(ZK_ECOMM, "no communicator attached");
@@ -396,26 +442,6 @@ inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   s.dev_out = via_rccl ? d_red(c) : nullptr;
   s.host_out = via_rccl ? nullptr : c->h_red;
   s.host_flag = via_rccl ? nullptr : h_flag(c);
-  return s;
-}
-
-// The 729-limb step (k_gkr_d0q): its own accumulator, all-reduce buffer and
-// pinned totals (the shared ones hold <= 256 u64), the same counters and flag.
-inline void ensure_wide(zk_ctx* c) {
-  if (!c->h_wide) {
-    c->wide.ensure(2 * zk::kWideSlot * 8);
-    HIPCK(hipMemset(c->wide.p, 0, 2 * zk::kWideSlot * 8));
-    HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_wide), zk::kWideSlot * 8, hipHostMallocMapped | hipHostMallocCoherent));
-    memset(c->h_wide, 0, zk::kWideSlot * 8);
-  }
-  c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kWideSlot * 8);
-}
-inline zk::RoundSink make_sink_wide(zk_ctx* c, bool across_ranks) {
-  zk::RoundSink s = make_sink(c, across_ranks);
-  uint64_t* w = reinterpret_cast<uint64_t*>(c->wide.p);
-  s.accum = w;
-  if (s.dev_out) s.dev_out = w + zk::kWideSlot;
-  if (s.host_out) s.host_out = c->h_wide;
   return s;
 }
 
@@ -448,19 +474,12 @@ inline void wait_flag(zk_ctx* c, uint32_t tag) {
 // ranks over RCCL the device totals are all-reduced and then published.
 inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
   if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
-    NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
+    {
+      CollTimer ct(c, 8.0 * n);
+      NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
+    }
     c->stats.collectives += 1;
     zk::k_publish<<<1, 256, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
-    HIPCK(hipGetLastError());
-  }
-}
-
-inline void enqueue_reduce_wide(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
-  if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
-    uint64_t* red = reinterpret_cast<uint64_t*>(c->wide.p) + zk::kWideSlot;
-    NCCLCK(ncclAllReduce(red, red, n, ncclUint64, ncclSum, c->nccl, c->stream));
-    c->stats.collectives += 1;
-    zk::k_publish<<<1, 256, 0, c->stream>>>(red, n, c->h_wide, h_flag(c), sk.tag);
     HIPCK(hipGetLastError());
   }
 }
@@ -478,30 +497,26 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
   uint64_t w[K * 17 > 17 ? K * 17 : 17];
   for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
   if (multi && c->comm == COMM_HOST) {
+    CollTimer ct(c, 8.0 * n);
     if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
     c->stats.collectives += 1;
   }
   for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w + L * k, L, L == 17 || product);
 }
 
-// the K x L limb sums of a 729-limb step (h_wide), summed over ranks when sharded
-template <class F, int K>
-void collect_wide(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, Fe (&out)[K]) {
-  const bool multi = across_ranks && multi_rank(c);
-  const int n = K * L;
-  wait_flag(c, sk.tag);
-  if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) != 0)
-    fail(ZK_EDEVICE, "a pre-enqueued round kernel waited more than 1 s for its challenge");
-  std::vector<uint64_t> w(n);
-  for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_wide + i, __ATOMIC_RELAXED);
-  if (multi && c->comm == COMM_HOST) {
-    if (c->ar(c->user, w.data(), n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
-    c->stats.collectives += 1;
-  }
-  for (int k = 0; k < K; ++k) out[k] = zk::hlimbs_to_fe<F>(w.data() + L * k, L, true);
+// Partial-sum slots (one kSlotU64 slot per block; above atomic_fanin the
+// grid also writes the 8 shard slots after its last block). Sized, before a
+// phase enqueues anything, for the largest grid a step over tables of 2^nv
+// elements can launch: a resident grid (<= 8 blocks of 256 threads per CU) or
+// the int32-tile minimum of the matrix-core steps (k_gkr_d0t: 2 ceil(2^nv /
+// 2^17) blocks; k_gkr_t33, k_gkr_dm3, k_gkr_dm and k_gkr_d0m need fewer).
+inline uint64_t max_step_grid(zk_ctx* c, uint32_t nv) {
+  const uint64_t tile = nv > 17 ? (uint64_t)2 << (nv - 17) : 2;
+  return std::max<uint64_t>((uint64_t)c->num_cus * 8, tile);
 }
-
-inline void ensure_partials(zk_ctx* c) { c->partials.ensure(((size_t)c->num_cus * 8 + 8) * zk::kSlotU64 * 8); }
+inline void ensure_partials(zk_ctx* c, uint32_t nv) {
+  c->partials.ensure((size_t)(max_step_grid(c, nv) + 8) * zk::kSlotU64 * 8);
+}
 
 // ---------------------------------------------------------------------------
 // GKR sum-check rounds
@@ -555,18 +570,25 @@ struct PostR {
     __atomic_store_n(&s->tag, tag, __ATOMIC_RELEASE);
   }
   // the double-round slot: 24 self-tagged words (tag << 32 | limb), any order
-  void post2(const Fe& ra, const Fe& rb, const Fe& rab, uint32_t tag) { post4(ra, rb, rab, zk::Fe{}, tag); }
-  // four values (a fold by four: the pending challenges, oldest first); every word carries the tag
-  void post4(const Fe& ra, const Fe& rb, const Fe& rc, const Fe& rd, uint32_t tag) {
+  void post2(const Fe& ra, const Fe& rb, const Fe& rab, uint32_t tag) {
     note();
     zk::RPost* s = h_rpost(c);
     const uint64_t t = (uint64_t)tag << 32;
     for (int i = 0; i < 8; ++i) {
       __atomic_store_n(&s->w[i], t | ra.v[i], __ATOMIC_RELAXED);
       __atomic_store_n(&s->w[8 + i], t | rb.v[i], __ATOMIC_RELAXED);
-      __atomic_store_n(&s->w[16 + i], t | rc.v[i], __ATOMIC_RELAXED);
-      __atomic_store_n(&s->w[24 + i], t | rd.v[i], __ATOMIC_RELAXED);
+      __atomic_store_n(&s->w[16 + i], t | rab.v[i], __ATOMIC_RELAXED);
     }
+  }
+  // the device-FS tail's first step: also the transcript digest and the claim (dfs.hpp kFsWords)
+  void post5(const Fe& ra, const Fe& rb, const Fe& rab, const uint32_t (&dig)[8], const Fe& claim, uint32_t tag) {
+    zk::RPost* s = h_rpost(c);
+    const uint64_t t = (uint64_t)tag << 32;
+    for (int i = 0; i < 8; ++i) {
+      __atomic_store_n(&s->w[24 + i], t | dig[i], __ATOMIC_RELAXED);
+      __atomic_store_n(&s->w[32 + i], t | claim.v[i], __ATOMIC_RELAXED);
+    }
+    post2(ra, rb, rab, tag);
   }
   ~PostR() {
     if (done || last == 0) return;
@@ -617,14 +639,11 @@ struct GStep {
   uint32_t i;      // first round (local)
   int np;          // double / dtail: pending challenges at entry (1 or 2)
   uint32_t nd = 0; // dtail: double steps it runs
+  bool dfs = false;  // dtail: device-side Fiat-Shamir between its steps (ZK_DEVICE_FS)
 };
 enum {
   GS_ROUND0 = 0, GS_SINGLE = 1, GS_DOUBLE = 2, GS_TAIL = 3, GS_DTAIL = 4, GS_D0 = 5, GS_D0T = 6, GS_T32 = 7, GS_T33 = 8,
-  GS_TT = 9,     // one small triple step (k_gkr_ttail, one step per launch)
-  GS_TTAIL = 10, // the small triple steps in one persistent kernel (k_gkr_ttail)
-  GS_HOST = 11,  // the last rounds on the host, from the tables the persistent tail's last step hands over
-  GS_D0Q = 12,   // rounds 0-3 over the inputs (k_gkr_d0q)
-  GS_T43 = 13    // fold by the four pending challenges + three rounds (k_gkr_t33<F, 64, 4>)
+  GS_HOST = 11   // the last rounds on the host, from the tables the persistent tail's last step hands over
 };
 
 // Host rounds (ZK_HOST_ROUNDS, default 4; only where the caller does not
@@ -682,62 +701,24 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   // persistent k_gkr_dtail). nt: the largest count leaving an even number
   // R >= 12 of rounds after the triples, else the smallest leaving an even
   // R >= 8 (every matrix-core step needs >= 64 quads / 32 octants).
-  // ZK_TTAIL=1 (measured slower, kept for A/B): triple steps to the end, the
-  // small ones in the persistent k_gkr_ttail, with 0-2 two-round steps so the
-  // rest is a multiple of three. Its one-wave-per-SIMD MFMA steps are
-  // latency-bound on tiny levels (~45 us per triple step against ~11 us per
-  // double step of k_gkr_dtail).
+  // (Measured and removed: triple steps to the end in a persistent MFMA
+  // kernel, and rounds 0-3 in the input pass with a fold by four)
   const bool d0t = c->dround && c->d0t && nv >= 11;
-  // ZK_D0Q: rounds 0-3 in the input pass (k_gkr_d0q) and a fold by four at
-  // level 4 (k_gkr_t33<F, 64, 4>: 1/16 of the tables written instead of 1/8),
-  // then the triple steps as after k_gkr_d0t from round 7. Needs >= 64
-  // octants at level 4 and no sharded cut before round 7.
-  bool d0q = d0t && c->d0q && !c->ttail && nv >= 15 && (gather_max == 0 || nv - 7 > gather_max);
   int nt = -1;
-  const int base = d0q ? 7 : 3;  // first round of the triple steps
-  if (d0t && !c->ttail)
-    for (int k = 0; base + 3 * k + 8 <= (int)nv; ++k) {
-      const int R = (int)nv - base - 3 * k;
+  if (d0t)
+    for (int k = 0; 3 + 3 * k + 8 <= (int)nv; ++k) {
+      const int R = (int)nv - 3 - 3 * k;
       if (R % 2 == 0 && (R >= 12 || nt < 0)) nt = k;
     }
-  if (d0q && nt < 0) d0q = false;
-  if (d0q) ensure_wide(c);  // (before anything of this phase is enqueued)
-  const bool d0t_doubles = d0t && !c->ttail && nt >= 0;
-  const bool d0t_triples = d0t && c->ttail;
-  const bool d0 = !d0t_doubles && !d0t_triples && c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
-  if (nv >= 1) steps.push_back({d0q ? GS_D0Q : (d0t_doubles || d0t_triples ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0)), 0, 0});
+  const bool d0t_doubles = d0t && nt >= 0;
+  const bool d0 = !d0t_doubles && c->dround && c->d0 > 0 && nv >= 2 && nv % 2 == 0;
+  if (nv >= 1) steps.push_back({d0t_doubles ? GS_D0T : (d0 ? GS_D0 : GS_ROUND0), 0, 0});
   if (d0t_doubles) {
-    if (d0q) steps.push_back({GS_T43, 4u, 4});
-    for (int k = 0; k < nt; ++k) steps.push_back({GS_T33, (uint32_t)base + 3u * k, 3});
-    steps.push_back({GS_T32, (uint32_t)base + 3u * nt, 3});
+    for (int k = 0; k < nt; ++k) steps.push_back({GS_T33, 3u + 3u * k, 3});
+    steps.push_back({GS_T32, 3u + 3u * nt, 3});
   }
-  if (d0t_triples) {
-    const int R = (int)nv - 3;
-    int a = 0;
-    while ((R - 2 * a) % 3 != 0) ++a;
-    int ntri = (R - 2 * a) / 3;
-    uint32_t i = 3;
-    while (ntri > 0 && (int)nv - (int)i >= 16) {
-      steps.push_back({GS_T33, i, 3});
-      i += 3;
-      --ntri;
-    }
-    for (int k = 0; k < a; ++k, i += 2) steps.push_back({k == 0 ? GS_T32 : GS_DOUBLE, i, k == 0 ? 3 : 2});
-    const int np0 = a > 0 ? 2 : 3;
-    if (ntri > 0 && pre && c->dtail && use_tail(c, across_ranks) && ntri <= 64) {
-      steps.push_back({GS_TTAIL, i, np0, (uint32_t)ntri});
-      const uint64_t O0 = (L >> i) / 8;
-      const size_t had = c->tailbuf.bytes;
-      c->tailbuf.ensure(kTailRelayBytes + zk::ttail_region(O0, (uint32_t)ntri) * sizeof(Fe));
-      if (c->tailbuf.bytes != had) HIPCK(hipMemset(c->tailbuf.p, 0, kTailRelayBytes));  // relay tags at rest
-    } else {
-      for (int k = 0; k < ntri; ++k, i += 3) steps.push_back({GS_TT, i, k == 0 ? np0 : 3});
-    }
-  }
-  if (d0t_triples) {
-    // (the schedule above covers every round)
-  } else if (c->dround) {
-    uint32_t i = d0t_doubles ? (uint32_t)base + 2u + 3u * nt : (d0 ? 2 : 1);
+  if (c->dround) {
+    uint32_t i = d0t_doubles ? 5u + 3u * nt : (d0 ? 2 : 1);
     int np = d0t_doubles || d0 ? 2 : 1;  // challenges pending at the first double step
     if (!d0 && !d0t_doubles) {
       if (nv >= 2) steps.push_back({GS_SINGLE, i++, 0});
@@ -771,7 +752,15 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       if (d0 < steps.size() && nd >= 2 && nd <= 64) {
         const GStep first = steps[d0];
         steps.resize(d0);
-        steps.push_back({GS_DTAIL, first.i, first.np, (uint32_t)nd});
+        // device-side Fiat-Shamir between the tail's steps: one rank's sums only
+        // (a sharded tail's sums are all-reduced on the host between steps)
+        const bool dfs = c->device_fs && !(across_ranks && multi_rank(c));
+        steps.push_back({GS_DTAIL, first.i, first.np, (uint32_t)nd, dfs});
+        if (dfs && !c->h_fslog) {
+          HIPCK(hipHostMalloc(reinterpret_cast<void**>(&c->h_fslog), 64 * sizeof(zk::FsLog),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+          memset(c->h_fslog, 0, 64 * sizeof(zk::FsLog));
+        }
         const uint64_t Q0 = (L >> first.i) / 4;
         const size_t had = c->tailbuf.bytes;
         c->tailbuf.ensure(kTailRelayBytes + zk::dtail_region(Q0, (uint32_t)nd) * sizeof(Fe));
@@ -814,10 +803,8 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   auto rounds_of = [&](const GStep& st) -> uint32_t {
     switch (st.kind) {
       case GS_DOUBLE: case GS_D0: case GS_T32: return 2;
-      case GS_D0T: case GS_T33: case GS_TT: case GS_T43: return 3;
-      case GS_D0Q: return 4;
+      case GS_D0T: case GS_T33: return 3;
       case GS_DTAIL: return 2 * st.nd;
-      case GS_TTAIL: return 3 * st.nd;
       case GS_TAIL: case GS_HOST: return nv - st.i;
       default: return 1;
     }
@@ -827,7 +814,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     for (size_t s = 0; s < steps.size(); ++s) {
       const uint32_t b = steps[s].i + rounds_of(steps[s]);
       const int k = steps[s].kind;
-      if (k == GS_TAIL || k == GS_DTAIL || k == GS_TTAIL || k == GS_HOST) break;  // (persistent steps are not cut)
+      if (k == GS_TAIL || k == GS_DTAIL || k == GS_HOST) break;  // (persistent steps are not cut)
       if (b < nv && nv - b <= gather_max) {
         steps.resize(s + 1);
         end = b;
@@ -848,7 +835,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
   std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
   int inbuf = -1;                        // work buffer holding cur (-1: the input tables)
-  Fe ry = zk::fe_zero<F>(), rz = ry, ra = ry, rb = ry;  // last four challenges (oldest first)
+  Fe rz = zk::fe_zero<F>(), ra = rz, rb = rz;  // last three challenges (oldest first)
   auto out_tables = [&](uint64_t size, Fe* nx[4]) {
     const int ob = inbuf == 0 ? 1 : 0;
     Fe* w = c->work[ob].fe();
@@ -861,7 +848,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint32_t i = st.i;
     const uint64_t size = L >> i;  // table length in round i
     const uint64_t h = size / 2;   // pairs
-    sinks[i] = st.kind == GS_D0Q ? make_sink_wide(c, across_ranks) : make_sink(c, across_ranks);
+    sinks[i] = make_sink(c, across_ranks);
     if (c->block_trace && (int)si == c->block_trace_step) sinks[i].btrace = c->block_trace;
     const zk::RoundSink& sk = sinks[i];
     if (st.kind == GS_ROUND0) {
@@ -872,19 +859,11 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     if (st.kind == GS_D0) {  // rounds 0 and 1 over the input tables (size 4Q), nothing written
       const uint64_t Q = size / 4;
-      if (c->d0 == 3) {  // products on the matrix cores (k_gkr_d0m, mfma.hpp)
-        const uint64_t nch = (Q + 31) / 32;
-        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_d0m<F>);
-        const uint32_t grid = step_grid(c, res, (nch + 2 * zk::kD0MChunksMax - 1) / (2 * zk::kD0MChunksMax));
-        launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0m<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
-      } else if (c->d0 == 2) {  // ZK_D0=2: the 8-lane k_gkr_d0 (DPP exchange, V11 in schoolbook rows)
-        const uint32_t grid = grid_for(c, zk::kDQuads * Q, zk::k_gkr_d0<F>);
-        launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
-      } else {  // a quad-product per three lanes, one grid row each (k_gkr_d0r)
-        const uint64_t threads = (2 * Q + zk::kD0RUnits - 1) / zk::kD0RUnits * 64;
-        const uint32_t grid = grid_for(c, threads, zk::k_gkr_d0r<F>);
-        launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0r<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
-      }
+      // products on the matrix cores (k_gkr_d0m, mfma.hpp)
+      const uint64_t nch = (Q + 31) / 32;
+      const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_d0m<F>);
+      const uint32_t grid = step_grid(c, res, (nch + 2 * zk::kD0MChunksMax - 1) / (2 * zk::kD0MChunksMax));
+      launch(c, ZK_K_GKR_D0, 128.0 * size, 4.5 * size, zk::k_gkr_d0m<F>, grid, cur[0], cur[1], cur[2], cur[3], Q, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0Limbs);
       return;
     }
@@ -896,65 +875,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
     }
-    if (st.kind == GS_D0Q) {  // rounds 0-3 over the input tables (size 16 H), nothing written
-      const uint64_t H = size / 16, nch = H / 32;
-      uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)c->num_cus, 2 * nch) & ~1u;  // one block per CU
-      if (c->grid_cap) grid = std::max<uint32_t>(2, std::min<uint32_t>(grid, c->grid_cap) & ~1u);
-      // a block takes at most kD0QDrain chunks (int32 tiles): more blocks than CUs beyond 24 variables
-      grid = std::max<uint32_t>(grid, (uint32_t)(2 * ((nch + zk::kD0QDrain - 1) / zk::kD0QDrain)));
-      launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0q<F>, grid, cur[0], cur[1], cur[2], cur[3], H, sk);
-      enqueue_reduce_wide(c, sk, across_ranks, zk::kD0QLimbs);
-      return;
-    }
-    if (st.kind == GS_TT || st.kind == GS_TTAIL) {  // small triple steps (k_gkr_ttail)
-      const uint64_t O0 = size / 8;
-      const uint32_t nd = st.kind == GS_TTAIL ? st.nd : 1u;
-      zk::TTailArgs a{};
-      for (int t = 0; t < 4; ++t) a.in[t] = cur[t];
-      a.O0 = O0;
-      a.nsteps = nd;
-      a.np0 = (uint32_t)st.np;
-      a.err = h_err(c);
-      uint32_t grid;
-      if (st.kind == GS_TTAIL) {
-        for (uint32_t d = 1; d < nd; ++d) sinks[i + 3 * d] = make_sink(c, across_ranks);
-        a.relay = reinterpret_cast<zk::RPost*>(c->tailbuf.p);
-        a.out = reinterpret_cast<Fe*>(reinterpret_cast<char*>(c->tailbuf.p) + kTailRelayBytes);
-        a.host = h_rpost(c);
-        rtags[si] = c->rtag + 1;
-        c->rtag += nd;
-        a.rtag0 = rtags[si];
-        if (c->tail_trace) a.trace = c->tail_trace;
-        grid = (uint32_t)std::min<uint64_t>((uint64_t)c->num_cus, (O0 + 31) / 32);  // one block per CU: co-resident
-      } else {
-        Fe* nx[4];
-        out_tables(size, nx);
-        a.out = nx[0];  // 4 tables of 8 O0 back to back
-        a.relay = d_rpost(c);
-        if (pre) {
-          a.host = h_rpost(c);
-          a.rtag0 = rtags[si] = ++c->rtag;
-        } else {
-          a.r[0] = rz;
-          a.r[1] = ra;
-          a.r[2] = rb;
-        }
-        grid = (uint32_t)std::min<uint64_t>((uint64_t)c->num_cus, (O0 + 31) / 32);
-      }
-      double bytes = 0, muls = 0;
-      for (uint32_t d = 0; d < nd; ++d) {
-        const double O = (double)(O0 >> (3 * d)), nw = d == 0 ? (double)(1u << st.np) : 8.0;
-        bytes += (nw * 8 + 8) * 4 * 32 * O;
-        muls += 96.0 * O;
-      }
-      launch(c, ZK_K_GKR_DTAIL, bytes, muls, zk::k_gkr_ttail<F>, grid, a, sk);
-      const uint64_t Ol = O0 >> (3 * (nd - 1));
-      Fe* last = a.out + zk::ttail_region(O0, nd - 1);
-      for (int t = 0; t < 4; ++t) cur[t] = last + (uint64_t)t * 8 * Ol;
-      if (st.kind == GS_TT) enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
-      return;
-    }
-    if (st.kind == GS_T32 || st.kind == GS_T33 || st.kind == GS_T43) {  // fold level i-3 (i-4) by three (four) challenges to level i
+    if (st.kind == GS_T32 || st.kind == GS_T33) {  // fold level i-3 by three challenges to level i
       const uint64_t Q = size / 4;
       Fe* nx[4];
       out_tables(size, nx);
@@ -964,25 +885,10 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.relay = d_rpost(c);
         din.err = h_err(c);
         din.tag = rtags[si] = ++c->rtag;
-      } else if (st.kind == GS_T43) {
-        din.ra = ry;
-        din.rb = rz;
-        din.rab = ra;
-        din.r4 = rb;
       } else {
         din.ra = rz;
         din.rb = ra;
         din.rab = rb;  // carries r_{i-1} for this step
-      }
-      if (st.kind == GS_T43) {  // rounds i .. i+2 over level i's octants, folded from level i-4
-        const uint64_t O = size / 8, nch = O / 64;
-        const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64, 4>);
-        const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
-        launch(c, ZK_K_GKR_T33, 17408.0 * O, 192.0 * O, zk::k_gkr_t33<F, 64, 4>, grid, cur[0], cur[1], cur[2], cur[3],
-               nx[0], nx[1], nx[2], nx[3], O, din, sk);
-        for (int t = 0; t < 4; ++t) cur[t] = nx[t];
-        enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
-        return;
       }
       if (st.kind == GS_T33) {  // rounds i .. i+2 over level i's octants: 27 moment sums
         const uint64_t O = size / 8;
@@ -1056,6 +962,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       a.rtag0 = rtags[si];
       if (c->tail_trace) a.trace = c->tail_trace;
       if (si + 1 < ns && steps[si + 1].kind == GS_HOST) a.host_tab = c->h_tab;
+      a.fslog = c->h_fslog;
       const uint32_t grid = (uint32_t)std::min<uint64_t>(
           {(Q0 + zk::kDQuads - 1) / zk::kDQuads, (uint64_t)std::min<uint32_t>(c->dtail_blocks, 64u), (uint64_t)c->num_cus});
       double bytes = 0, muls = 0;
@@ -1064,7 +971,10 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         bytes += (two ? 2560.0 : 1536.0) * (Q0 >> (2 * d));
         muls += (two ? 40.0 : 24.0) * (Q0 >> (2 * d));
       }
-      launch(c, ZK_K_GKR_DTAIL, bytes, muls, zk::k_gkr_dtail<F>, std::max<uint32_t>(grid, 1u), a, sk);
+      if (st.dfs)
+        launch(c, ZK_K_GKR_DTAIL, bytes, muls, zk::k_gkr_dtail<F, true>, std::max<uint32_t>(grid, 1u), a, sk);
+      else
+        launch(c, ZK_K_GKR_DTAIL, bytes, muls, zk::k_gkr_dtail<F, false>, std::max<uint32_t>(grid, 1u), a, sk);
       const uint64_t Ql = Q0 >> (2 * (st.nd - 1));
       Fe* last = a.out + zk::dtail_region(Q0, st.nd - 1);
       for (int t = 0; t < 4; ++t) cur[t] = last + (uint64_t)t * 4 * Ql;
@@ -1136,7 +1046,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   // the highest challenge tag step si (and every step before it) waits for
   auto last_tag = [&](size_t si) {
     if (steps[si].kind == GS_TAIL) return rtags[si] + (nv - steps[si].i) - 1;
-    if (steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL) return rtags[si] + steps[si].nd - 1;
+    if (steps[si].kind == GS_DTAIL) return rtags[si] + steps[si].nd - 1;
     return rtags[si];
   };
   PostR post{c};
@@ -1155,10 +1065,19 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     if (!pre || si + 1 >= ns) return;
     const GStep& nx = steps[si + 1];
     if (nx.kind == GS_HOST) return;
-    if (nx.kind == GS_T43) {
-      post.post4(ry, rz, ra, rb, rtags[si + 1]);
-    } else if (nx.kind == GS_T32 || nx.kind == GS_T33 || nx.kind == GS_TT || nx.kind == GS_TTAIL) {
+    if (nx.kind == GS_T32 || nx.kind == GS_T33) {
       post.post2(rz, ra, rb, rtags[si + 1]);
+    } else if (nx.kind == GS_DTAIL && nx.dfs) {
+      // the sponge after a challenge is the zero state + its 32-byte digest
+      // buffered (dfs.hpp): the device continues the transcript from there
+      const zk::Keccak256& h = tr->h;
+      bool fresh = h.fill == 32;
+      for (int q = 0; q < 25; ++q) fresh = fresh && h.st[q] == 0;
+      if (!fresh) fail(ZK_EINVAL, "internal: device Fiat-Shamir needs a transcript right after a challenge");
+      uint32_t dig[8];
+      memcpy(dig, h.buf, 32);
+      const Fe rab = nx.np == 2 ? zk::hfe_mul<F>(ra, rb) : zk::fe_zero<F>();
+      post.post5(nx.np == 2 ? ra : zk::fe_zero<F>(), rb, rab, dig, claim, rtags[si + 1]);
     } else if (nx.kind == GS_DOUBLE || nx.kind == GS_DTAIL) {
       if (nx.np == 2)
         post.post2(ra, rb, zk::hfe_mul<F>(ra, rb), rtags[si + 1]);
@@ -1170,7 +1089,6 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   };
   auto one_round = [&](uint32_t i, const Fe& e0, const Fe& e1, const Fe& e2) {
     claim = finish_round<F>(tr, e0, e1, e2, k0 + i, out, r);
-    ry = rz;
     rz = ra;
     ra = rb;
     rb = r;
@@ -1219,61 +1137,6 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     one_round(i0 + 2, Z[0], hfe_sub<F>(claim, Z[0]), at2w(Z[0], Z[1], Z[2]));
   };
-  // rounds i0 .. i0 + 3 from the 81 moment sums of k_gkr_d0q (27 t0 + 9 b + 3 c + d;
-  // t0: 0, 1, inf along the first variable, b, c, d: 0, 1, s as in three_rounds)
-  auto four_rounds = [&](uint32_t i0, bool first) {
-    using namespace zk;
-    Fe T[kD0QCats];
-    collect_wide<F, kD0QCats>(c, sinks[i0], across_ranks, 9, T);
-    for (int j = 0; j < 27; ++j) T[54 + j] = hfe_sub<F>(hfe_add<F>(T[j], T[27 + j]), T[54 + j]);  // X0 Y1 + X1 Y0
-    const Fe one = fe_one<F>(), two = hfe_add<F>(one, one), four = hfe_add<F>(two, two);
-    auto at2w = [&](const Fe (&m)[3]) { return hfe_sub<F>(hfe_add<F>(m[0], hfe_mul<F>(four, m[1])), hfe_mul<F>(two, m[2])); };
-    auto wts = [&](const Fe& t, Fe (&w)[3]) {
-      const Fe omt = hfe_sub<F>(one, t);
-      w[0] = hfe_mul<F>(omt, omt);
-      w[1] = hfe_mul<F>(t, t);
-      w[2] = hfe_mul<F>(t, omt);
-    };
-    auto dot3 = [&](const Fe (&w)[3], const Fe& x0, const Fe& x1, const Fe& x2) {  // one reduction
-      uint64_t acc[9] = {0};
-      h64::mac_wide(acc, h64::of(w[0]), h64::of(x0));
-      h64::mac_wide(acc, h64::of(w[1]), h64::of(x1));
-      h64::mac_wide(acc, h64::of(w[2]), h64::of(x2));
-      return wide_to_fe<F>(acc);
-    };
-    auto at = [&](int a, int b, int cc, int d) -> const Fe& { return T[27 * a + 9 * b + 3 * cc + d]; };
-    Fe S3[3][3][3], S2[3][3], U[3];  // sums over the trailing variables' hypercube points (moments 0 and 1)
-    for (int a = 0; a < 3; ++a) {
-      for (int b = 0; b < 3; ++b) {
-        for (int cc = 0; cc < 3; ++cc) S3[a][b][cc] = hfe_add<F>(at(a, b, cc, 0), at(a, b, cc, 1));
-        S2[a][b] = hfe_add<F>(S3[a][b][0], S3[a][b][1]);
-      }
-      U[a] = hfe_add<F>(S2[a][0], S2[a][1]);
-    }
-    one_round(i0, U[0], first ? U[1] : hfe_sub<F>(claim, U[0]), at2w(U));
-    Fe wa[3];
-    wts(r, wa);
-    Fe V[3];
-    for (int b = 0; b < 3; ++b) V[b] = dot3(wa, S2[0][b], S2[1][b], S2[2][b]);
-    one_round(i0 + 1, V[0], hfe_sub<F>(claim, V[0]), at2w(V));
-    Fe wb[3];
-    wts(r, wb);
-    Fe W2[3][3], Z[3];
-    for (int b = 0; b < 3; ++b)
-      for (int cc = 0; cc < 3; ++cc) W2[b][cc] = dot3(wa, S3[0][b][cc], S3[1][b][cc], S3[2][b][cc]);
-    for (int cc = 0; cc < 3; ++cc) Z[cc] = dot3(wb, W2[0][cc], W2[1][cc], W2[2][cc]);
-    one_round(i0 + 2, Z[0], hfe_sub<F>(claim, Z[0]), at2w(Z));
-    Fe wc[3];
-    wts(r, wc);
-    Fe W3[3][3][3], Wb[3][3], Q[3];
-    for (int b = 0; b < 3; ++b)
-      for (int cc = 0; cc < 3; ++cc)
-        for (int d = 0; d < 3; ++d) W3[b][cc][d] = dot3(wa, at(0, b, cc, d), at(1, b, cc, d), at(2, b, cc, d));
-    for (int cc = 0; cc < 3; ++cc)
-      for (int d = 0; d < 3; ++d) Wb[cc][d] = dot3(wb, W3[0][cc][d], W3[1][cc][d], W3[2][cc][d]);
-    for (int d = 0; d < 3; ++d) Q[d] = dot3(wc, Wb[0][d], Wb[1][d], Wb[2][d]);
-    one_round(i0 + 3, Q[0], hfe_sub<F>(claim, Q[0]), at2w(Q));
-  };
   // rounds i0 and i0 + 1 from a double step's eight product sums (the first
   // step of a phase, k_gkr_d0: nine, the ninth V11 for round 0's e1)
   auto two_rounds = [&](uint32_t i0, bool first = false) {
@@ -1316,23 +1179,11 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     } else if (st.kind == GS_D0T) {
       three_rounds(0, true);
       pend = 3;
-    } else if (st.kind == GS_D0Q) {
-      four_rounds(0, true);
-      pend = 4;
-    } else if (st.kind == GS_T43) {
-      three_rounds(st.i, false);
-      pend = 3;
     } else if (st.kind == GS_T32) {
       two_rounds(st.i);
       pend = 2;
-    } else if (st.kind == GS_T33 || st.kind == GS_TT) {
+    } else if (st.kind == GS_T33) {
       three_rounds(st.i, false);
-      pend = 3;
-    } else if (st.kind == GS_TTAIL) {
-      for (uint32_t d = 0; d < st.nd; ++d) {
-        three_rounds(st.i + 3 * d, false);
-        if (d + 1 < st.nd) post.post2(rz, ra, rb, rtags[si] + d + 1);
-      }
       pend = 3;
     } else if (st.kind == GS_SINGLE) {
       Fe s2[2];
@@ -1384,6 +1235,38 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(),
                 std::chrono::duration<double, std::micro>(t1 - t0).count());
       pend = 0;
+    } else if (st.dfs) {  // GS_DTAIL, device Fiat-Shamir: steps 0 .. nd-2 drew their own challenges
+      // their records are complete once the last step's flag is up (every
+      // logging wave drained first, kernels.hpp k_gkr_dtail): replay them into
+      // the host transcript — absorb the device's coefficients, draw the
+      // challenge, check it against the device's — then finish the last step
+      wait_flag(c, sinks[st.i + 2 * (st.nd - 1)].tag);
+      for (uint32_t d = 0; d + 1 < st.nd; ++d) {
+        const zk::FsLog& lg = c->h_fslog[d];
+        if (__atomic_load_n(&lg.tag, __ATOMIC_ACQUIRE) != rtags[si] + d)
+          fail(ZK_EDEVICE, "device Fiat-Shamir record missing");
+        for (int j = 0; j < 2; ++j) {
+          Fe cf[3], rd;
+          for (int q = 0; q < 3; ++q) memcpy(cf[q].v, lg.c[j][q], 32);
+          memcpy(rd.v, lg.r[j], 32);
+          const uint32_t m = lg.m[j];
+          if (m > 3) fail(ZK_EDEVICE, "device Fiat-Shamir record corrupt");
+          const uint32_t k = k0 + st.i + 2 * d + j;
+          absorb<F>(tr, cf, m);
+          out.ncoeffs[k] = (uint8_t)m;
+          for (uint32_t q = 0; q < 3; ++q) out.coeffs[3 * k + q] = q < m ? cf[q] : zk::fe_zero<F>();
+          r = challenge<F>(tr);
+          if (memcmp(r.v, rd.v, 32) != 0) fail(ZK_EDEVICE, "device Fiat-Shamir challenge differs from the host transcript");
+          out.challenges[k] = r;
+          claim = zk::hfe_add<F>(cf[0], zk::hfe_mul<F>(r, zk::hfe_add<F>(cf[1], zk::hfe_mul<F>(r, cf[2]))));
+          c->stats.device_fs_rounds += 1;
+          rz = ra;
+          ra = rb;
+          rb = r;
+        }
+      }
+      two_rounds(st.i + 2 * (st.nd - 1));
+      pend = 2;
     } else {  // GS_DTAIL
       for (uint32_t d = 0; d < st.nd; ++d) {
         two_rounds(st.i + 2 * d);
@@ -1399,10 +1282,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const uint64_t* T = c->tail_trace + 512;
     uint64_t prev_pub = 0;
     for (size_t si = 0; si < ns; ++si) {
-      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_TTAIL || steps[si].kind == GS_HOST) break;
+      if (steps[si].kind == GS_TAIL || steps[si].kind == GS_DTAIL || steps[si].kind == GS_HOST) break;
       const uint64_t* row = T + (sinks[steps[si].i].tag & 63) * 4;
-      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T ||
-                         steps[si].kind == GS_D0Q;  // no challenge to wait for
+      const bool first = steps[si].kind == GS_ROUND0 || steps[si].kind == GS_D0 || steps[si].kind == GS_D0T;  // no challenge to wait for
       const uint64_t rr = first ? row[0] : row[1];
       fprintf(stderr, "zk step %zu (kind %d, round %u): publish->entry %7.2f us, entry->r %7.2f, r->publish %8.2f"
               " (r->block 0 loop end %8.2f, ->publish %6.2f)\n", si, steps[si].kind, steps[si].i,
@@ -1458,16 +1340,6 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
               m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
               (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, m + 1 < nr ? (T[m * 8 + 9] - T[m * 8 + 4]) * 0.01 : 0.0);
   }
-  if (c->tail_trace && !steps.empty() && steps.back().kind == GS_TTAIL) {  // ZK_DEBUG_TAIL
-    HIPCK(hipStreamSynchronize(c->stream));
-    const uint64_t* T = c->tail_trace;
-    const uint32_t nd = steps.back().nd;
-    for (uint32_t m = 0; m < nd; ++m)
-      fprintf(stderr, "zk ttail step %u: wait r %6.2f us, constants %6.2f, fold+products %6.2f, epilogue %6.2f, fan-in+publish %6.2f, hand-off to next r %6.2f\n",
-              m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
-              (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, (T[m * 8 + 5] - T[m * 8 + 4]) * 0.01,
-              m + 1 < nd ? (T[m * 8 + 9] - T[m * 8 + 5]) * 0.01 : 0.0);
-  }
   const size_t sdt = !steps.empty() && steps.back().kind == GS_HOST ? steps.size() - 2 : steps.size() - 1;
   if (c->tail_trace && !steps.empty() && steps[sdt].kind == GS_DTAIL) {  // ZK_DEBUG_TAIL
     HIPCK(hipStreamSynchronize(c->stream));
@@ -1491,7 +1363,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
   out.ncoeffs.assign(n, 0);
   out.challenges.assign(n, zk::fe_zero<F>());
   if (n == 0) return;
-  ensure_partials(c);
+  ensure_partials(c, nloc);
   __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
   const uint64_t Lloc = (uint64_t)1 << nloc;
   const uint64_t wmax = std::max<uint64_t>(Lloc / 2, (uint64_t)G);
@@ -1546,6 +1418,7 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
       for (int t = 0; t < 4; ++t) cur[t] = dst + t * dstride;
     }
     if (c->comm == COMM_RCCL) {  // in place: this rank's slot is its send buffer
+      CollTimer ct(c, 4.0 * Tn * 32);
       NCCLCK(ncclAllGather(slot, oh, (size_t)4 * Tn * 4, ncclUint64, c->nccl, c->stream));
       c->stats.collectives += 1;
     } else {
@@ -1611,7 +1484,7 @@ void sc_prove_device(zk_ctx* c, const Fe* dX, uint32_t n, zk_transcript* tr, con
   // The transcript absorbs the whole table first (sum_check_protocol.rs:27):
   // a serial host Keccak. Round 0's half sums (and, pre-enqueued, every later
   // round) are launched before it so the GPU works underneath the hash.
-  ensure_partials(c);
+  ensure_partials(c, n);
   __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
   const uint64_t N = (uint64_t)1 << n;
   if (n == 0) {

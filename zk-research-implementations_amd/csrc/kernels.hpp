@@ -9,6 +9,7 @@
 // per-lane access (two dwordx4).
 #pragma once
 #include "field.hpp"
+#include "dfs.hpp"
 
 namespace zk {
 
@@ -21,6 +22,13 @@ __device__ __forceinline__ Fe ld_fe(const Fe* __restrict__ p, uint64_t i) {
   r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
   r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
   return r;
+}
+// a pointer the compiler cannot prove wave-uniform (selected by the wave
+// index), made uniform: its address arithmetic stays on the scalar unit
+__device__ __forceinline__ const Fe* uniform_ptr(const Fe* p) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return reinterpret_cast<const Fe*>(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ void st_fe(Fe* __restrict__ p, uint64_t i, const Fe& x) {
   uint4* q = reinterpret_cast<uint4*>(p) + 2 * i;
@@ -837,32 +845,26 @@ __global__ __launch_bounds__(kBlock) void k_gkr_tail(TailArgs a, RoundSink sink)
 // between the words is needed.
 // ---------------------------------------------------------------------------
 struct alignas(64) RPost {
-  uint64_t w[32];  // up to four values; the two-round slot uses words 0-23
+  uint64_t w[40];  // ra, rb, rab in words 0-23; the device-FS tail also the digest (24-31) and the claim (32-39)
 };
 struct DIn {
   Fe ra, rb, rab;      // used as is when host == null
-  Fe r4;               // (four-challenge steps: the newest challenge; ra, rb, rab the older three)
   const RPost* host;   // pinned slot the host posts to, or null
   RPost* relay;        // device relay slot (used when gridDim > 1)
   uint32_t* err;       // pinned error word
   uint32_t tag;
 };
-template <int NV = 3>
-__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab, bool relay, Fe* r4 = nullptr) {
-  static_assert(NV == 3 || NV == 4, "three or four posted values");
-  if (!in.host) {
-    ra = in.ra;
-    rb = in.rb;
-    rab = in.rab;
-    if (NV == 4) *r4 = in.r4;
-    return;
-  }
-  __shared__ uint32_t s_w[8 * NV];
+// NV tagged values (8 words each) into s_w[8 NV] (LDS; valid after the barrier).
+// Block 0 polls the host slot and copies the words to the device relay when
+// `relay`; the other blocks poll the relay. dev_only: every block polls the
+// relay, which a previous step's device-side Fiat-Shamir wrote (dfs.hpp).
+template <int NV>
+__device__ __forceinline__ void block_get_words(const DIn& in, uint32_t* s_w, bool relay, bool dev_only) {
   if (threadIdx.x < 64) {  // wave 0
     const uint32_t lane = threadIdx.x;
     const bool mine = lane < 8 * NV;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const bool direct = blockIdx.x == 0;
+    const bool direct = blockIdx.x == 0 && !dev_only;
     uint64_t v = 0;
     bool ok = true;
     while (true) {
@@ -879,12 +881,21 @@ __device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& 
     if (mine) s_w[lane] = (uint32_t)v;
   }
   __syncthreads();
+}
+__device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& rab, bool relay) {
+  if (!in.host) {
+    ra = in.ra;
+    rb = in.rb;
+    rab = in.rab;
+    return;
+  }
+  __shared__ uint32_t s_w[24];
+  block_get_words<3>(in, s_w, relay, false);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     ra.v[i] = s_w[i];
     rb.v[i] = s_w[8 + i];
     rab.v[i] = s_w[16 + i];
-    if (NV == 4) r4->v[i] = s_w[24 + i];
   }
 }
 
@@ -1007,173 +1018,14 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dround(const Fe* __restrict__ A,
   grid_finish<kDLimbs>(sc, sink);
 }
 
-// ---------------------------------------------------------------------------
-// Rounds 0 and 1 from the input tables in one pass (even round counts). With
-// nothing to fold, the quad's corners are the inputs themselves; round 0 needs
-// e0 = sum V00^2 + V01^2, e1 = sum V10^2 + V11^2, e2 = sum V20^2 + V21^2 and
-// round 1 the two quadratics through V(.,0) and V(.,2): all nine grid points,
-// the eight of k_gkr_dround plus the corner V11 (category 8). Its product is
-// split over the unit's 8 lanes, lane u = 4 tab + k forming schoolbook row u
-// (V11_A times word u of V11_S); the row sums are shifted by u words when the
-// block sums them (d0_limb_sums). Nothing is written: the next step folds the
-// inputs by (r_0, r_1) at once.
-// ---------------------------------------------------------------------------
+// Rounds 0 and 1 from the input tables in one pass (even round counts,
+// k_gkr_d0m in mfma.hpp): nothing to fold, so the quad's corners are the
+// inputs themselves; round 0 needs e0, e1, e2 and round 1 the two quadratics
+// through V(.,0) and V(.,2) — all nine grid points, the eight of a double step
+// plus the corner V11 (category 8). The next step folds the inputs by
+// (r_0, r_1) at once.
 constexpr int kD0Cats = 9;
 constexpr int kD0Limbs = kD0Cats * 17;  // 153 limb sums
-struct D0Scratch {
-  uint32_t rows[kBlock * 27];  // 17 words of the eight-point accumulator + 10 of the row accumulator
-  uint64_t tot[kSlotU64];
-  uint64_t pp[kBlock];
-  uint32_t am_last;
-};
-template <class F>
-__global__ __launch_bounds__(kBlock) void k_gkr_d0(const Fe* __restrict__ A, const Fe* __restrict__ S,
-                                                   const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t Q,
-                                                   RoundSink sink) {
-  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
-  __shared__ D0Scratch sc;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1, u = lane & 7;
-  const uint32_t pp = wv & 1, jl = (wv >> 1) * 8 + (lane >> 3);
-  const Fe* __restrict__ X = pp ? (tab ? P : M) : (tab ? S : A);
-  Wide acc = wide_zero<F>();
-  uint32_t row[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // sum of this lane's schoolbook rows of V11_A V11_S
-  for (uint64_t jb = (uint64_t)blockIdx.x * kDQuads; jb < Q; jb += (uint64_t)gridDim.x * kDQuads) {
-    const uint64_t j = jb + jl;
-    if (j < Q) {  // uniform over the 8 lanes of a unit
-      const Fe q = ld_fe(X, j + k * Q);
-      unit_product<F>(q, k, tab, acc);
-      const Fe own3 = dpp_fe<kQP3333>(q), other3 = xor4_fe(own3);  // V11 of this table, of the other
-      const Fe xa = tab ? other3 : own3, ys = tab ? own3 : other3;  // A side, S side
-      uint32_t yu = ys.v[0];
-#pragma unroll
-      for (int w = 1; w < 8; ++w) yu = u == (uint32_t)w ? ys.v[w] : yu;
-      uint64_t Pw[8];
-#pragma unroll
-      for (int w = 0; w < 8; ++w) Pw[w] = (uint64_t)xa.v[w] * yu;
-      uint32_t prod[9], c = 0;  // the 288-bit row, then row += prod
-      prod[0] = (uint32_t)Pw[0];
-#pragma unroll
-      for (int w = 1; w < 8; ++w) prod[w] = addc32((uint32_t)Pw[w], (uint32_t)(Pw[w - 1] >> 32), c, &c);
-      prod[8] = (uint32_t)(Pw[7] >> 32) + c;
-      c = 0;
-#pragma unroll
-      for (int w = 0; w < 9; ++w) row[w] = addc32(row[w], prod[w], c, &c);
-      row[9] += c;
-    }
-  }
-  // limb sums: categories 0..7 as k_gkr_dround; category 8 = sum over lanes of row << 32 u
-#pragma unroll
-  for (int w = 0; w < 17; ++w) sc.rows[threadIdx.x * 27 + w] = acc.w[w];
-#pragma unroll
-  for (int w = 0; w < 10; ++w) sc.rows[threadIdx.x * 27 + 17 + w] = row[w];
-  __syncthreads();
-  const uint32_t t = threadIdx.x;
-  if (t < (uint32_t)kDLimbs) {
-    const uint32_t c = t / 17, w = t % 17, uu = 4 * (c & 1) + (c >> 1);
-    uint64_t s0 = 0;
-    for (uint32_t m = 0; m < kBlock / 8; ++m) s0 += sc.rows[(8 * m + uu) * 27 + w];
-    sc.tot[t] = s0;
-  } else if (t < (uint32_t)kD0Limbs) {
-    const uint32_t w = t - kDLimbs;  // column w of category 8
-    uint64_t s0 = 0;
-    for (uint32_t r = 0; r < (uint32_t)kBlock; ++r) {
-      const int src = (int)w - (int)(r & 7u);
-      if (src >= 0 && src < 10) s0 += sc.rows[r * 27 + 17 + src];
-    }
-    sc.tot[t] = s0;
-  }
-  __syncthreads();
-  grid_finish<kD0Limbs>(sc, sink);
-}
-
-// Extended grid point 2 hi - lo. For fields with 3p < 2^256 (BN254) it is lazy,
-// 2 hi + (p - lo) in [0, 3p): product sums of such operands stay exact
-// integers congruent mod p (the consumer reduces 17-word totals of any size,
-// hlimbs_to_fe). lo must be reduced.
-template <class F>
-constexpr bool kLazyExt = (uint64_t)F::P[7] * 3 + 3 < (1ull << 32);
-template <class F>
-__device__ __forceinline__ Fe ext2(const Fe& lo, const Fe& hi) {  // 2 hi - lo (mod p), lo < p
-  if constexpr (kLazyExt<F>) {
-    Fe d, r;
-    uint32_t b = 0, c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) d.v[i] = subb32(F::P[i], lo.v[i], b, &b);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = addc32(hi.v[i], hi.v[i], c, &c);
-    c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.v[i] = addc32(r.v[i], d.v[i], c, &c);
-    return r;
-  } else {
-    return at2<F>(lo, hi);
-  }
-}
-// ---------------------------------------------------------------------------
-// k_gkr_d0r: a quad-product per THREE lanes, lane a forming grid row a
-// (points (a,0), (a,1), (a,2)): rows 0 and 1 start from the corners, row 2
-// from V(2,b) = 2 V(1,b) - V(0,b) (reduced), and V(a,2) = ext2(V(a,0), V(a,1)).
-// Nine products over nine slots (no empty slot), three accumulators per lane
-// (fewer VGPRs, more waves per SIMD); 21 units per wave, lane 63 idle.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kD0RUnits = 21;                // units per wave
-constexpr uint32_t kD0RQuads = 2 * kD0RUnits;     // quads per block iteration (2 waves per product)
-template <class F>
-__global__ __launch_bounds__(kBlock, 2) void k_gkr_d0r(const Fe* __restrict__ A, const Fe* __restrict__ S,
-                                                      const Fe* __restrict__ M, const Fe* __restrict__ P,
-                                                      uint64_t Q, RoundSink sink) {
-  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
-  __shared__ DScratch sc;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t unit = (lane * 43u) >> 7, a = lane - 3 * unit;  // lane / 3, lane % 3 for lane < 64
-  const uint32_t pp = wv & 1, jl = (wv >> 1) * kD0RUnits + unit;
-  const Fe* __restrict__ X = pp ? M : A;
-  const Fe* __restrict__ Z = pp ? P : S;
-  Wide acc[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) acc[s] = wide_zero<F>();
-  if (unit < kD0RUnits) {
-    for (uint64_t jb = (uint64_t)blockIdx.x * kD0RQuads; jb < Q; jb += (uint64_t)gridDim.x * kD0RQuads) {
-      const uint64_t j = jb + jl;
-      if (j < Q) {  // uniform over the 3 lanes of a unit
-        const Fe x00 = ld_fe(X, j), x01 = ld_fe(X, j + Q), x10 = ld_fe(X, j + 2 * Q), x11 = ld_fe(X, j + 3 * Q);
-        const Fe z00 = ld_fe(Z, j), z01 = ld_fe(Z, j + Q), z10 = ld_fe(Z, j + 2 * Q), z11 = ld_fe(Z, j + 3 * Q);
-        __builtin_amdgcn_sched_barrier(0);  // issue all loads before any arithmetic
-        const Fe x0 = a == 2 ? at2<F>(x00, x10) : sel_fe(a == 0, x00, x10);
-        const Fe z0 = a == 2 ? at2<F>(z00, z10) : sel_fe(a == 0, z00, z10);
-        wide_mac<F>(acc[0], x0, z0);
-        const Fe x1 = a == 2 ? at2<F>(x01, x11) : sel_fe(a == 0, x01, x11);
-        const Fe z1 = a == 2 ? at2<F>(z01, z11) : sel_fe(a == 0, z01, z11);
-        wide_mac<F>(acc[1], x1, z1);
-        wide_mac<F>(acc[2], ext2<F>(x0, x1), ext2<F>(z0, z1));
-      }
-    }
-  }
-  // block limb sums, one slot (column b of the grid) at a time; category of point (a, b):
-  // 0 V00, 1 V22, 2 V01, 3 V02, 4 V10, 5 V20, 6 V21, 7 V12, 8 V11 (host.hpp two_rounds)
-  constexpr int kCat[3][3] = {{0, 2, 3}, {4, 8, 7}, {5, 6, 1}};
-  const uint32_t t = threadIdx.x;
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-#pragma unroll
-    for (int w = 0; w < 17; ++w) sc.rows[t * 17 + w] = acc[b].w[w];
-    __syncthreads();
-    if (t < 204) {  // wave part (t / 51) sums its 21 lanes of row ra
-      const uint32_t part = t / 51, r = t % 51, ra = r / 17, w = r % 17;
-      uint64_t s0 = 0;
-#pragma unroll 7
-      for (uint32_t u = 0; u < kD0RUnits; ++u) s0 += sc.rows[(part * 64 + 3 * u + ra) * 17 + w];
-      sc.pp[t] = s0;
-    }
-    __syncthreads();
-    if (t < 51) {
-      const uint32_t ra = t / 17, w = t % 17;
-      sc.tot[kCat[ra][b] * 17 + w] = sc.pp[t] + sc.pp[51 + t] + sc.pp[102 + t] + sc.pp[153 + t];
-    }
-    __syncthreads();
-  }
-  grid_finish<kD0Limbs>(sc, sink);
-}
 
 // ---------------------------------------------------------------------------
 // The small double rounds of a proof in ONE persistent kernel: step s is the
@@ -1200,6 +1052,7 @@ struct DTailArgs {
   uint32_t* err;      // pinned error word
   uint64_t* trace;    // debug (ZK_DEBUG_TAIL): per step 8 s_memrealtime stamps, or null
   uint64_t* host_tab; // pinned host memory: the last step's 4 output tables (16 Q elements), or null (host-side rounds)
+  FsLog* fslog;       // (DFS) pinned: per step but the last, the rounds the device drew (dfs.hpp)
 };
 __host__ __device__ __forceinline__ uint64_t dtail_region(uint64_t Q0, uint32_t s) {
   uint64_t o = 0;
@@ -1221,10 +1074,19 @@ __device__ __forceinline__ void st_fe_sys(uint64_t* p, uint64_t n, uint64_t i, c
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <class F>
+// DFS (ZK_DEVICE_FS=1, dfs.hpp): every step but the last draws the next
+// step's challenges on the device. The host posts step 0's (ra, rb, rab), the
+// transcript digest and the running claim; after each later step's sums the
+// block that counts in last runs both rounds' Fiat-Shamir on wave 0 (dfs_double)
+// and writes the next step's words to its relay slot (tagged, agent scope),
+// which every block polls — no host round trip inside the tail. The host
+// replays the logged rounds into its transcript afterwards and compares the
+// challenges; the last step publishes its sums as usual.
+template <class F, bool DFS>
 __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sink) {
   __shared__ DScratch sc;
   __shared__ Fe ct[30];
+  __shared__ uint32_t s_w[kFsWords];  // (DFS) the step's relay words
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, k = lane & 3, tab = (lane >> 2) & 1;
   const uint32_t pp = wv & 1, jl = (wv >> 1) * 8 + (lane >> 3);
   const uint32_t tb = 2 * pp + tab;  // table A, S, M, P
@@ -1232,7 +1094,10 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     const uint64_t Q = a.Q0 >> (2 * st);
     const uint64_t want = (Q + kDQuads - 1) / kDQuads;
     const uint32_t nb = want < gridDim.x ? (uint32_t)want : gridDim.x;
-    if (blockIdx.x >= nb) return;  // idle from here on (nb never grows)
+    if (blockIdx.x >= nb) {  // idle from here on (nb never grows)
+      if (DFS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a logged step's host stores land before the final flag
+      return;
+    }
     DIn din{};
     din.host = a.host;
     din.relay = a.relay + st;
@@ -1240,7 +1105,17 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     din.tag = a.rtag0 + st;
     Fe ra, rb, rab;
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-    block_get_rs(din, ra, rb, rab, nb > 1);
+    if constexpr (DFS) {
+      block_get_words<kFsWords / 8>(din, s_w, nb > 1, st > 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ra.v[i] = s_w[i];
+        rb.v[i] = s_w[8 + i];
+        rab.v[i] = s_w[16 + i];
+      }
+    } else {
+      block_get_rs(din, ra, rb, rab, nb > 1);
+    }
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 1] = __builtin_amdgcn_s_memrealtime();
     const bool two = st > 0 || a.np0 == 2;
     fold_consts<F, 3>(ra, rb, rab, ct);  // blocks 0, 1, 2: ra, rb, ra rb
@@ -1275,6 +1150,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     RoundSink sk = sink;
     sk.tag = sink.tag + st;
     const uint32_t t = threadIdx.x;
+    bool last = true;  // this block holds the step's totals in sc.tot
     if (nb > 1) {
       if (t < (uint32_t)kDLimbs) __hip_atomic_fetch_add(sk.accum + t, sc.tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1284,17 +1160,38 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
         sc.am_last = prev == nb - 1;
       }
       __syncthreads();
-      if (sc.am_last) {
+      last = sc.am_last;
+      if (last) {
         if (t < (uint32_t)kDLimbs)
           sc.tot[t] = __hip_atomic_exchange(sk.accum + t, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (a.trace && t == 0) a.trace[st * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-        publish_limbs<kDLimbs>(sc, sk);
-        if (a.trace && t == 0) a.trace[st * 8 + 5] = __builtin_amdgcn_s_memrealtime();
       }
-    } else {
+    }
+    if (last) {
       if (a.trace && t == 0) a.trace[st * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-      publish_limbs<kDLimbs>(sc, sk);
+      if (DFS && st + 1 < a.nsteps) {
+        __syncthreads();  // sc.tot complete
+        if (t < 64) {  // wave 0: both rounds' Fiat-Shamir, then the next step's relay words
+          __shared__ DfsScratch dsc;
+          Fe claim, rr[3];
+          uint32_t dig[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            dig[i] = s_w[24 + i];
+            claim.v[i] = s_w[32 + i];
+          }
+          dfs_double<F>(sc.tot, claim, dig, rr, a.fslog + st, dsc);
+          if (t < (uint32_t)kFsWords) {
+            const uint32_t q = t & 7, g = t >> 3;
+            const uint32_t v = g == 0 ? rr[0].v[q] : g == 1 ? rr[1].v[q] : g == 2 ? rr[2].v[q] : g == 3 ? dig[q] : claim.v[q];
+            __hip_atomic_store(&a.relay[st + 1].w[t], ((uint64_t)(din.tag + 1) << 32) | v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (t == 0) __hip_atomic_store(&a.fslog[st].tag, din.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      } else {
+        publish_limbs<kDLimbs>(sc, sk);
+      }
       if (a.trace && t == 0) a.trace[st * 8 + 5] = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();  // sc is reused next step

@@ -758,364 +758,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
 
 
 // ---------------------------------------------------------------------------
-// k_gkr_d0q: rounds 0-3 in ONE pass over the input tables (ZK_D0Q), so that
-// the first fold pass folds by four challenges and writes 1/16 of the tables
-// instead of 1/8 (DESIGN.md §3a'': the first fold pass is bound by its
-// read:write mix, and its writes are the lever). Along variable 0 a table
-// is written at the points 0, 1 and "infinity" (X(inf) = X1 - X0, the
-// leading coefficient of X(t) = X0 + t (X1 - X0); |X(inf)| < p keeps valid
-// signed digits for every field); per point t0 the products X(t0) Y(t0) over
-// the 8 x 8 corner pairs of variables 1-3 go to 27 moment tiles exactly as in
-// k_gkr_d0t: 81 tiles, indexed 27 t0 + 9 d1 + 3 d2 + d3 (d: 0 = X0 Y0,
-// 1 = X1 Y1, 2 = X0 Y1 + X1 Y0). The host (four_rounds) turns the t0 = inf
-// moment into the s moment: X0 Y1 + X1 Y0 = m0 + m1 - m_inf.
-// Block b serves product b & 1. Lane (table, group) of every wave loads two
-// of the group's eight corner pairs (the next chunk's loads in flight while
-// this one is converted), forms the inf values and writes 3 digit rows per
-// pair into a double-buffered image [t0][corner of variables 1-3][table][32
-// groups][32 B] (48 KiB per buffer); the chunk's 192 products are split over
-// the four waves (48 each, at most 21 tiles, d0q_group), one wave per SIMD.
-// (A first version had one wave convert all eight pairs for three waves of
-// 27 tiles: issue-bound, 0.8 ms per pass at 24 variables.) One barrier per
-// chunk: the waves fill buffer k & 1 and multiply buffer (k - 1) & 1. int32 bound: a slot takes at most 8 MFMAs
-// per chunk (2^22), so a block takes at most kD0QDrain chunks (the host sizes
-// the grid: beyond 24 variables it exceeds one block per CU).
-// Output: 81 x 9 limb sums (grid_finish_wide).
-// ---------------------------------------------------------------------------
-constexpr int kD0QCats = 81;
-constexpr int kD0QLimbs = kD0QCats * 9;  // 729
-constexpr int kWideSlot = 768;           // per-block slot of grid_finish_wide (u64)
-constexpr uint32_t kD0QDrain = 256;      // chunks per block at most (the host sizes the grid; one drain at the end)
-static_assert(8ull * (1u << 19) * kD0QDrain <= (1ull << 30), "d0q tile bound");
-struct D0QEpi {
-  uint64_t w17[kD0QCats][17];
-  uint64_t tot[kWideSlot];
-  uint64_t pp[kBlock];
-  uint32_t am_last;
-};
-struct D0QScratch {
-  union {
-    uint8_t img[2][3][8][2][32][32];  // buffer, t0, corner (variables 1-3), table, group, digit row: 96 KiB
-    D0QEpi e;                         // epilogue (after the main loop)
-  };
-  unsigned long long T[kD0QCats][64];  // int64 anti-diagonal sums
-  uint32_t p2w[9][8];
-};
-
-// grid_finish for C > kBlock limb sums (sc.tot[0..C), every thread's share):
-// per-block slots of kWideSlot u64, the same two-level fan-in (or u64 atomics
-// for small grids) and publication as grid_finish.
-template <int C, class Sc>
-__device__ __forceinline__ void grid_finish_wide(Sc& sc, const RoundSink& sk) {
-  static_assert(C <= kWideSlot, "limb vector too long");
-  const uint32_t G = gridDim.x, t = threadIdx.x;
-  ZK_BLOCK_STAMP(sk, 1);
-  auto publish = [&]() {
-    for (uint32_t q = t; q < (uint32_t)C; q += kBlock) {
-      const uint64_t v = sc.tot[q];
-      if (sk.dev_out) sk.dev_out[q] = v;
-      if (sk.host_out) __hip_atomic_store(sk.host_out + q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ZK_SINK_STAMP(sk, 2);
-    __syncthreads();  // every storing wave has drained before the flag
-    if (t == 0 && sk.host_flag) __hip_atomic_store(sk.host_flag, sk.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  };
-  if (G == 1) {
-    publish();
-    return;
-  }
-  if (G <= sk.atomic_max) {
-    for (uint32_t q = t; q < (uint32_t)C; q += kBlock)
-      __hip_atomic_fetch_add(sk.accum + q, sc.tot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) sc.am_last = __hip_atomic_fetch_add(sk.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
-    __syncthreads();
-    ZK_BLOCK_STAMP(sk, 2);
-    if (!sc.am_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t q = t; q < (uint32_t)C; q += kBlock)
-      sc.tot[q] = __hip_atomic_exchange(sk.accum + q, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == 0) __hip_atomic_store(sk.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    publish();
-    return;
-  }
-  auto sum_slots_wide = [&](uint32_t first, uint32_t stride, uint32_t count) {
-    for (uint32_t q = t; q < (uint32_t)C; q += kBlock) {
-      uint64_t s = 0;
-      uint32_t i = 0;
-      for (; i + 8 <= count; i += 8) {
-        uint64_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld_u64_sc1(sk.partials + (uint64_t)(first + (i + u) * stride) * kWideSlot + q);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
-      }
-      for (; i < count; ++i) s += ld_u64_sc1(sk.partials + (uint64_t)(first + i * stride) * kWideSlot + q);
-      sc.tot[q] = s;
-    }
-  };
-  const uint32_t shard = blockIdx.x & 7u, nshards = G < 8 ? G : 8u;
-  const uint32_t in_shard = (G - shard + 7u) / 8u;
-  for (uint32_t q = t; q < (uint32_t)C; q += kBlock) st_u64_sc1(sk.partials + (uint64_t)blockIdx.x * kWideSlot + q, sc.tot[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0)
-    sc.am_last = __hip_atomic_fetch_add(sk.counter + 32 * shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 in_shard - 1;
-  __syncthreads();
-  ZK_BLOCK_STAMP(sk, 2);
-  if (!sc.am_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  sum_slots_wide(shard, 8u, in_shard);
-  for (uint32_t q = t; q < (uint32_t)C; q += kBlock) st_u64_sc1(sk.partials + (uint64_t)(G + shard) * kWideSlot + q, sc.tot[q]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __hip_atomic_store(sk.counter + 32 * shard, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sc.am_last = __hip_atomic_fetch_add(sk.counter + 32 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nshards - 1;
-  }
-  __syncthreads();
-  if (!sc.am_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  sum_slots_wide(G, 1u, nshards);
-  if (t == 0) __hip_atomic_store(sk.counter + 32 * 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  publish();
-}
-
-// The 192 products of a chunk (64 corner pairs (U, V) of variables 1-3 per
-// point t0) and the 81 tiles they feed are split over the four waves so that
-// every wave takes 48 products and at most 21 tiles, leaving registers for
-// two of the chunk's eight pairs of loads per lane: wave w < 3 takes point
-// t0 = w except the tiles with d1 = s, d2 != s (21 tiles: local group
-// g = 3 d1 + d2 for d1 < 2, g = 6 for (s, s)); wave 3 takes exactly those
-// (t0, s, d2 < 2) tiles of every point (18 tiles: g = 2 t0 + d2). Local tile
-// 3 g + d3. The tiles' register files are fixed here (the first 16 in AGPRs,
-// the rest in VGPRs): left to itself the allocator spills whole tiles every
-// chunk, and a spill of an inline-asm MFMA's result would race the MFMA.
-template <int SLOT>
-__device__ __forceinline__ void d0q_mfma(i32x16& acc, const i32x4& a, const i32x4& b) {
-  if constexpr (SLOT < 16)
-    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-  else
-    asm volatile("v_mfma_i32_32x32x32_i8 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-__host__ __device__ constexpr int d0q_group(int role, int t0, int d1, int d2) {
-  return role == 0 ? (d1 < 2 ? 3 * d1 + d2 : (d2 == 2 ? 6 : -1)) : (d1 == 2 && d2 < 2 ? 2 * t0 + d2 : -1);
-}
-template <int ROLE, int T0, int U, int V, int NT>
-__device__ __forceinline__ void d0q_prod(i32x16 (&acc)[NT], const i32x4& fa, const i32x4& fb) {
-  constexpr int d1 = moment_digit(U >> 2, V >> 2), d2 = moment_digit((U >> 1) & 1, (V >> 1) & 1);
-  constexpr int g = d0q_group(ROLE, T0, d1, d2);
-  if constexpr (g >= 0) {
-    constexpr int slot = 3 * g + moment_digit(U & 1, V & 1);
-    d0q_mfma<slot>(acc[slot], fa, fb);
-  }
-}
-template <int ROLE, int T0, int U, int VH, int NT>
-__device__ __forceinline__ void d0q_row(i32x16 (&acc)[NT], const i32x4& fa, const i32x4 (&fb)[4]) {
-  d0q_prod<ROLE, T0, U, 4 * VH + 0>(acc, fa, fb[0]);
-  d0q_prod<ROLE, T0, U, 4 * VH + 1>(acc, fa, fb[1]);
-  d0q_prod<ROLE, T0, U, 4 * VH + 2>(acc, fa, fb[2]);
-  d0q_prod<ROLE, T0, U, 4 * VH + 3>(acc, fa, fb[3]);
-}
-// Wave w < 3 (ROLE 0): the products of its point's image img = [corner][table]
-// [32][32] with Y corners 4 VH .. 4 VH + 3: rows with u1 = VH take 4 products,
-// the others 2; X fragments are read two rows ahead (three in registers) so
-// a 2-product row does not wait for its read (the MFMAs are volatile asm: the
-// scheduler does not hoist reads above them on its own).
-template <int VH, int NT>
-__device__ __forceinline__ void d0q_half(const uint8_t (*img)[2][32][32], i32x16 (&acc)[NT]) {
-  i32x4 fb[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) fb[v] = tr_frag(&img[4 * VH + v][1][0][0]);
-  i32x4 f0 = tr_frag(&img[0][0][0][0]), f1 = tr_frag(&img[1][0][0][0]), f2 = tr_frag(&img[2][0][0][0]);
-  d0q_row<0, 0, 0, VH>(acc, f0, fb);
-  f0 = tr_frag(&img[3][0][0][0]);
-  d0q_row<0, 0, 1, VH>(acc, f1, fb);
-  f1 = tr_frag(&img[4][0][0][0]);
-  d0q_row<0, 0, 2, VH>(acc, f2, fb);
-  f2 = tr_frag(&img[5][0][0][0]);
-  d0q_row<0, 0, 3, VH>(acc, f0, fb);
-  f0 = tr_frag(&img[6][0][0][0]);
-  d0q_row<0, 0, 4, VH>(acc, f1, fb);
-  f1 = tr_frag(&img[7][0][0][0]);
-  d0q_row<0, 0, 5, VH>(acc, f2, fb);
-  d0q_row<0, 0, 6, VH>(acc, f0, fb);
-  d0q_row<0, 0, 7, VH>(acc, f1, fb);
-}
-// Wave 3 (ROLE 1): stage (T0, VH) = the products X_U Y_V of point T0 with
-// v1 = VH, u1 = 1 - VH, u2 = v2 (8 products over 4 X and 4 Y fragments);
-// img3 = the whole buffer [t0][corner][table][32][32]. A stage's fragments are
-// read while the previous stage multiplies (two register sets).
-struct D0QFrags {
-  i32x4 a[4], b[4];
-};
-template <int T0, int VH>
-__device__ __forceinline__ void d0q_stage_load(const uint8_t (*img3)[8][2][32][32], D0QFrags& f) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f.a[r] = tr_frag(&img3[T0][4 * (1 - VH) + r][0][0][0]);
-#pragma unroll
-  for (int v = 0; v < 4; ++v) f.b[v] = tr_frag(&img3[T0][4 * VH + v][1][0][0]);
-}
-template <int T0, int VH, int R, int NT>
-__device__ __forceinline__ void d0q_stage_row(i32x16 (&acc)[NT], const D0QFrags& f) {
-  d0q_prod<1, T0, 4 * (1 - VH) + R, 4 * VH + 2 * (R >> 1)>(acc, f.a[R], f.b[2 * (R >> 1)]);
-  d0q_prod<1, T0, 4 * (1 - VH) + R, 4 * VH + 2 * (R >> 1) + 1>(acc, f.a[R], f.b[2 * (R >> 1) + 1]);
-}
-template <int T0, int VH, int NT>
-__device__ __forceinline__ void d0q_stage(i32x16 (&acc)[NT], const D0QFrags& f) {
-  d0q_stage_row<T0, VH, 0>(acc, f);
-  d0q_stage_row<T0, VH, 1>(acc, f);
-  d0q_stage_row<T0, VH, 2>(acc, f);
-  d0q_stage_row<T0, VH, 3>(acc, f);
-}
-template <int NT>
-__device__ __forceinline__ void d0q_role1(const uint8_t (*img3)[8][2][32][32], i32x16 (&acc)[NT]) {
-  D0QFrags f0, f1;
-  d0q_stage_load<0, 0>(img3, f0);
-  d0q_stage_load<0, 1>(img3, f1);
-  d0q_stage<0, 0>(acc, f0);
-  d0q_stage_load<1, 0>(img3, f0);
-  d0q_stage<0, 1>(acc, f1);
-  d0q_stage_load<1, 1>(img3, f1);
-  d0q_stage<1, 0>(acc, f0);
-  d0q_stage_load<2, 0>(img3, f0);
-  d0q_stage<1, 1>(acc, f1);
-  d0q_stage_load<2, 1>(img3, f1);
-  d0q_stage<2, 0>(acc, f0);
-  d0q_stage<2, 1>(acc, f1);
-}
-// local tile i of a wave -> category 27 t0 + 9 d1 + 3 d2 + d3
-__device__ __forceinline__ uint32_t d0q_cat(int role, uint32_t w, int i) {
-  const int g = i / 3, d3 = i % 3;
-  if (role == 0) {
-    const int d1 = g < 6 ? g / 3 : 2, d2 = g < 6 ? g % 3 : 2;
-    return 27u * w + (uint32_t)(9 * d1 + 3 * d2 + d3);
-  }
-  return (uint32_t)(27 * (g >> 1) + 18 + 3 * (g & 1) + d3);
-}
-// tiles -> the block's int64 anti-diagonal sums
-template <int ROLE, int NT>
-__device__ __forceinline__ void d0q_drain(i32x16 (&acc)[NT], unsigned long long (&T)[kD0QCats][64], uint32_t w) {
-  // the MFMAs above are inline asm: the hazard recognizer does not see their
-  // result latency, so wait it out (>= 18 wait states for a 16-pass MFMA) before reading
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  const uint32_t l = threadIdx.x & 63, col = l & 31, h = l >> 5;
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const uint32_t cat = d0q_cat(ROLE, w, i);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const uint32_t row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      atomicAdd(&T[cat][row + col], (unsigned long long)(long long)acc[i][r]);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // one tile at a time (all widened values would go live at once)
-  }
-}
-
-// pair q of group j (corners q and 8 + q along variable 0) of one table
-__device__ __forceinline__ void d0q_load(const Fe* __restrict__ X, uint64_t j, uint64_t H, int q, Fe (&x)[2]) {
-  x[0] = ld_fe(X, j + (uint64_t)q * H);
-  x[1] = ld_fe(X, j + (uint64_t)(8 + q) * H);
-}
-// the pair's three digit rows: t0 = 0, 1, inf (X(inf) = X1 - X0 in (-p, p))
-__device__ __forceinline__ void d0q_put(uint8_t (*img)[8][2][32][32], int q, uint32_t tb, uint32_t g, Fe (&x)[2]) {
-  Fe d = sub256(x[1], x[0]);
-  to_digits(d);
-  st_row(&img[2][q][tb][g][0], d);
-  to_digits(x[0]);
-  st_row(&img[0][q][tb][g][0], x[0]);
-  to_digits(x[1]);
-  st_row(&img[1][q][tb][g][0], x[1]);
-}
-
-// One wave's main loop: lane (table tb, group g) converts pairs 2w, 2w + 1 of
-// every chunk (the next chunk's loads in flight while this one is converted)
-// into image k (buffer k & 1) while the wave multiplies image k - 1; one
-// barrier per iteration (nk + 1 iterations for every wave).
-template <int ROLE>
-__device__ __forceinline__ void d0q_wave(D0QScratch& sc, const Fe* __restrict__ X, uint64_t H, uint64_t nch,
-                                         uint64_t nk, uint64_t ch0, uint64_t nb, uint32_t w, uint32_t tb, uint32_t g) {
-  constexpr int NT = ROLE == 0 ? 21 : 18;
-  i32x16 acc[NT];
-#pragma unroll
-  for (int i = 0; i < NT; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0;
-  auto jk = [&](uint64_t k) {  // group g of chunk ch0 + k nb (chunk 0 for a block without chunks)
-    const uint64_t c = ch0 + k * nb;
-    return (c < nch ? c : 0) * 32 + g;
-  };
-  auto products = [&](uint32_t b) {  // of the image in buffer b
-    if constexpr (ROLE == 0) {
-      d0q_half<0>(sc.img[b][w], acc);
-      d0q_half<1>(sc.img[b][w], acc);
-    } else {
-      d0q_role1(sc.img[b], acc);
-    }
-  };
-  // the next chunk's loads are never conditional (past the last chunk a wave
-  // loads it again): conditional loads made the compiler drain every load
-  // before the products, so no load was in flight during them
-  // two chunks in flight: buffers A (even k) and B (odd k), the loop unrolled
-  // by two so that no register copy waits for a load; iterations past nk
-  // (at most one) only load and meet the barrier
-  Fe ca[2][2], cb[2][2];
-  const uint64_t k1 = nk > 1 ? 1 : 0;
-  d0q_load(X, jk(0), H, 2 * (int)w, ca[0]);
-  d0q_load(X, jk(0), H, 2 * (int)w + 1, ca[1]);
-  d0q_load(X, jk(k1), H, 2 * (int)w, cb[0]);
-  d0q_load(X, jk(k1), H, 2 * (int)w + 1, cb[1]);
-  auto step = [&](uint64_t k, Fe (&cur)[2][2]) {
-    const uint64_t kn = k + 2 < nk ? k + 2 : (nk > 0 ? nk - 1 : 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      Fe x[2] = {cur[i][0], cur[i][1]};
-      d0q_load(X, jk(kn), H, 2 * (int)w + i, cur[i]);
-      if (k < nk) d0q_put(sc.img[k & 1], 2 * (int)w + i, tb, g, x);
-    }
-    if (k >= 1 && k <= nk) products((uint32_t)((k - 1) & 1));
-    __syncthreads();  // image k complete; image k - 1 consumed
-  };
-  for (uint64_t k = 0; k <= nk; k += 2) {  // nk <= kD0QDrain (the host sizes the grid)
-    step(k, ca);
-    step(k + 1, cb);
-  }
-  d0q_drain<ROLE>(acc, sc.T, w);
-}
-
-template <class F>
-__global__ __launch_bounds__(kBlock, 1) void k_gkr_d0q(const Fe* __restrict__ A, const Fe* __restrict__ S,
-                                                      const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t H,
-                                                      RoundSink sink) {
-  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
-  __shared__ D0QScratch sc;
-  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  for (uint32_t i = t; i < kD0QCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
-  stage_p2w<F>(sc.p2w);
-  const uint32_t pp = blockIdx.x & 1;
-  const uint64_t nch = H / 32, nb = gridDim.x >> 1, ch0 = blockIdx.x >> 1;
-  const uint64_t nk = ch0 < nch ? (nch - 1 - ch0) / nb + 1 : 0;  // this block's chunks: ch0 + k nb
-  __syncthreads();
-  const uint32_t tb = l >> 5, g = l & 31;
-  const Fe* __restrict__ X = tb ? (pp ? P : S) : (pp ? M : A);
-  if (w < 3)
-    d0q_wave<0>(sc, X, H, nch, nk, ch0, nb, w, tb, g);
-  else
-    d0q_wave<1>(sc, X, H, nch, nk, ch0, nb, w, tb, g);
-  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 3);  // block 0 leaves its main loop
-  ZK_BLOCK_STAMP(sink, 0);
-  __syncthreads();  // every drain is in T; the image is free for the epilogue
-  tiles_to_words<F, kD0QCats>(sc.T, sc.e.w17);
-  words_to_limbs9<F, kD0QCats>(sc.e.w17, sc.p2w, sc.e.tot);
-  __syncthreads();
-  grid_finish_wide<kD0QLimbs>(sc.e, sink);
-}
-
-// ---------------------------------------------------------------------------
 // k_gkr_dm3: the double step after k_gkr_d0t — THREE pending challenges
 // (ra, rb, rc) = (r_{i-3}, r_{i-2}, r_{i-1}). The level-(i-3) tables fold to
 // level i in one pass by the multilinear extension's own weights:
@@ -1250,44 +892,46 @@ struct T33Scratch {
   uint64_t pp[kBlock];
   uint32_t am_last;
   uint32_t p2w[9][8];  // 2^(32 (8 + k)) mod p, staged at kernel start for words_to_limbs9
-  Fe eqw[16];
+  Fe eqw[8];
 };
 
-// NP = 3: the fold by the three pending challenges (after k_gkr_d0t or a
-// previous triple step); NP = 4: by four (k_gkr_t43, after k_gkr_d0q): 16
-// inputs per output, K = 512, the 16 eq weights, and one fold's inputs in
-// flight instead of two (the same bytes), OCT 64 only.
-template <class F, int OCT, int NP = 3>
+template <class F, int OCT>
 __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
                                                       Fe* __restrict__ P2, uint64_t O, DIn din, RoundSink sink) {
-  static_assert(NP == 3 || (NP == 4 && OCT == 64), "fold by three, or by four with 64-octant chunks");
-  constexpr int NI = 1 << NP;  // inputs per output
-  Fe ra, rb, rc, rd;
+  constexpr int NI = 8;  // inputs per output
+  Fe ra, rb, rc;
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
-  const Fe* __restrict__ X = w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P));
+  const Fe* __restrict__ X = uniform_ptr(w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P)));
   Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
   const uint64_t nch = O / OCT, h8 = 8 * O;  // level-i tables hold 8 O elements
-  // fold f's inputs: OCT 64: corner f of octants ch*64 + l; OCT 32: corner 2f + hh of octants ch*32 + ql
+  // A fold of a chunk past the block's last one (the prefetch two folds
+  // ahead) loads chunk 0 instead: the load stays unconditional (a conditional
+  // load made hipcc drain every load at each chunk boundary) and every block's
+  // stray loads hit the same L2-resident lines (loading the block's own chunk
+  // again reached HBM: 1.13 x the algorithmic bytes at two chunks per block).
+  // (Measured and dropped: the same through bounds-checked buffer loads, which
+  // read zeros without an access — the 8 descriptors cost the kernel 16 VGPR
+  // spills and 11 SGPR spills, 512 vs 470 us for the first launch.)
+  // OCT 32: fold f = corners 2f (lanes 0-31) and 2f + 1 (lanes 32-63) of octants ch*32 + ql
   auto in_at = [&](uint64_t ch, int f, Fe (&x)[NI]) {
-    const uint64_t e = OCT == 64 ? ch * 64 + l + (uint64_t)f * O : ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
+    ch = ch < nch ? ch : 0;
+    const uint64_t e = ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
 #pragma unroll
     for (int k = 0; k < NI; ++k) x[k] = ld_fe(X, e + k * h8);
   };
-  // Inputs two units of eight ahead (one wave per SIMD: the loads in flight
-  // are what hides HBM latency); OCT 64 streams units (a fold by three: one
-  // unit per fold, by four: two; unit u = U f + h holds inputs 8 h .. 8 h + 7
-  // of fold f), OCT 32 whole folds. OCT 64: the first two units (written by
+  // Inputs two folds ahead (one wave per SIMD: the loads in flight are what
+  // hides HBM latency). OCT 64: the first two units (written by
   // the previous kernel) are in flight while the host posts the challenges
   // (OCT 32 loads them after the constants: held across them it spills).
   // Block 0's wave 0 polls the host for the challenges and relays them to
   // every block: its poll would wait behind these loads (vmcnt is in order),
   // so it loads after the challenges arrive.
-  constexpr int U = NI / 8;
-  auto unit_at = [&](uint64_t ch, int u, Fe (&x)[8]) {
-    const uint64_t e = ch * 64 + l + (uint64_t)(u / U) * O + (uint64_t)(8 * (u % U)) * h8;
+  auto unit_at = [&](uint64_t ch, int u, Fe (&x)[8]) {  // OCT 64: the eight inputs of fold u (corner u of octants ch*64 + l)
+    ch = ch < nch ? ch : 0;
+    const uint64_t e = ch * 64 + l + (uint64_t)u * O;
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
   };
@@ -1297,25 +941,18 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     unit_at(blockIdx.x, 0, nx);
     unit_at(blockIdx.x, 1, nx2);
   }
-  // the third word group carries rc for this step; a fold by four reads a fourth group
-  if constexpr (NP == 4)
-    block_get_rs<4>(din, ra, rb, rc, gridDim.x > 1, &rd);
-  else
-    block_get_rs(din, ra, rb, rc, gridDim.x > 1);
+  block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc for this step
   if (OCT == 64 && !early && (uint64_t)blockIdx.x < nch) {
     unit_at(blockIdx.x, 0, nx);
     unit_at(blockIdx.x, 1, nx2);
   }
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ T33Scratch sc;
-  if (t < (uint32_t)NI) {  // eq(r, c), the oldest pending challenge on c's top bit: c = 4a + 2b + c0 (+ d below)
+  if (t < (uint32_t)NI) {  // eq(r, c), the oldest pending challenge on c's top bit: c = 4a + 2b + c0
     const Fe one = fe_one<F>();
-    const uint32_t c3 = NP == 4 ? t >> 1 : t;  // the three older challenges' bits
-    const Fe fa = (c3 & 4) ? ra : fe_sub<F>(one, ra), fb = (c3 & 2) ? rb : fe_sub<F>(one, rb);
-    const Fe fc = (c3 & 1) ? rc : fe_sub<F>(one, rc);
-    Fe e = fe_mul<F>(fe_mul<F>(fa, fb), fc);
-    if constexpr (NP == 4) e = fe_mul<F>(e, (t & 1) ? rd : fe_sub<F>(one, rd));
-    sc.eqw[t] = e;
+    const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
+    const Fe fc = (t & 1) ? rc : fe_sub<F>(one, rc);
+    sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
   }
   for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
   stage_p2w<F>(sc.p2w);
@@ -1340,24 +977,19 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       i32x16 a0, a1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0;
-#pragma unroll
-      for (int h = 0; h < U; ++h) {
+      {
         Fe x[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           x[k] = nx[k];
           nx[k] = nx2[k];
         }
-        // the unit two ahead; past the block's last chunk its own chunk again
-        // (L2-hot): loads that are not conditional keep the compiler's vmcnt
-        // waits exact (a conditional load made it drain every load at each
-        // chunk boundary)
-        const int u2 = U * f + h + 2;
-        if (u2 < 8 * U)
+        const int u2 = f + 2;  // the fold two ahead
+        if (u2 < 8)
           unit_at(ch, u2, nx2);
         else
-          unit_at(ch + gridDim.x < nch ? ch + gridDim.x : ch, u2 - 8 * U, nx2);
-        fold_acc8(x, &wf[8 * h], a0, a1);
+          unit_at(ch + gridDim.x, u2 - 8, nx2);
+        fold_acc8(x, wf, a0, a1);
       }
       int64_t W[8];
       fold_words(a0, a1, W);
@@ -1404,8 +1036,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       }
       if (f < 2)
         in_at(ch, f + 2, nx2);
-      else if (ch + gridDim.x < nch)
-        in_at(ch + gridDim.x, f - 2, nx2);
+      else
+        in_at(ch + gridDim.x, f - 2, nx2);  // unconditional (past the end: chunk 0, L2-resident)
       const uint32_t corner = 2 * f + hh;
       const Fe z = dm3_fold<F>(x, wf);
       st_fold(X2, ch * 32 + ql + (uint64_t)corner * O, z);
@@ -1442,172 +1074,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   words_to_limbs9<F, kD0TCats>(sc.w17, sc.p2w, sc.tot);
   __syncthreads();
   grid_finish<kD0TLimbs>(sc, sink);
-}
-
-
-// ---------------------------------------------------------------------------
-// k_gkr_ttail: the small triple steps of a proof in ONE persistent kernel
-// (one block per CU, all co-resident). Step s is a k_gkr_t33 step over
-// O0 >> 3s octants: fold by the pending challenges (step 0: np0 = 2 or 3,
-// then 3) and sum three rounds as 27 moment tiles. No launch sits between
-// steps (each kernel boundary costs ~10 us on the box); per step block 0
-// waits for the host's challenges (three self-tagged groups, tag rtag0 + s:
-// r_{i-3}, r_{i-2}, r_{i-1}; a two-challenge fold uses the last two) and
-// relays them through a fresh slot, min(grid, chunks) blocks fold and
-// multiply, and grid_finish over those blocks publishes (sink tag tag0 + s).
-// Tables written in step s are read by other blocks in step s+1: every store
-// and load of them is an 8-byte agent-scope atomic (sc1), every storing wave
-// drains before its block counts in, each step writes a fresh region
-// (MI355X_MICROARCH.md "Valid forms"), as k_gkr_dtail (step 0's inputs, from
-// the previous kernel, are read the same way). Octants past O (O < 32) are
-// zero lanes: every lane stays active for the transposed reads.
-// ---------------------------------------------------------------------------
-struct TTailArgs {
-  const Fe* in[4];    // step 0 inputs: 2^np0 * 8 O0 elements per table (level i0 - np0)
-  Fe* out;            // step s writes 4 tables of 8 (O0 >> 3s) at out + ttail_region(O0, s)
-  uint64_t O0;        // octants of step 0's level
-  uint32_t nsteps;
-  uint32_t np0;       // pending challenges at step 0 (2 or 3)
-  uint32_t rtag0;     // challenge tag awaited by step 0
-  const RPost* host;  // pinned challenge words
-  RPost* relay;       // nsteps fresh relay slots
-  uint32_t* err;      // pinned error word
-  Fe r[3];            // the challenges when host == null (one step launched after them)
-  uint64_t* trace;    // debug (ZK_DEBUG_TAIL): per step 8 s_memrealtime stamps of block 0, or null
-};
-#define ZK_TT_STAMP(tr, st, k) \
-  do { if ((tr) && blockIdx.x == 0 && threadIdx.x == 0) (tr)[(st) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-__host__ __device__ __forceinline__ uint64_t ttail_region(uint64_t O0, uint32_t s) {
-  uint64_t o = 0;
-  for (uint32_t t = 0; t < s; ++t) o += 32 * (O0 >> (3 * t));
-  return o;
-}
-struct TTScratch {
-  uint8_t img[2][8][4][32][32];  // buffer, corner, table, octant, digit row (64 KiB)
-  unsigned long long T[kD0TCats][64];
-  uint64_t w17[kD0TCats][17];
-  uint64_t tot[kSlotU64];
-  uint64_t pp[kBlock];
-  uint32_t am_last;
-  uint32_t p2w[9][8];  // 2^(32 (8 + k)) mod p, staged at kernel start for words_to_limbs9
-  Fe eqw[8];
-};
-
-// one step of k_gkr_ttail with np pending challenges r[3 - np .. 2]; the block is
-// active. np = 2 runs as the three-challenge fold with the weights of inputs
-// 4..7 zero (and those inputs not loaded): one code path.
-template <class F>
-__device__ __forceinline__ void ttail_step(TTScratch& sc, const Fe (&r)[3], uint32_t np, const Fe* __restrict__ X,
-                                           Fe* __restrict__ X2, uint64_t O, uint32_t nb, const RoundSink& sk,
-                                           uint64_t* trace, uint32_t st) {
-  constexpr int NP = 3, NW = 8;
-  const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
-  const uint32_t nw = 1u << np;  // inputs per output
-  if (t < (uint32_t)NW) {  // eq((r_{3-np}, ..., r_2), c) for c < 2^np, else 0
-    const Fe one = fe_one<F>();
-    Fe e = one;
-    for (uint32_t b = 0; b < np; ++b) {
-      const Fe& rb = r[3 - np + b];
-      const bool bit = (t >> (np - 1 - b)) & 1;
-      e = fe_mul<F>(e, bit ? rb : fe_sub<F>(one, rb));
-    }
-    sc.eqw[t] = t < nw ? e : fe_zero<F>();
-  }
-  for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
-  __syncthreads();
-  uint8_t(*wimg)[32][32] = reinterpret_cast<uint8_t(*)[32][32]>(&sc.img[0][0][0][0][0]);
-  dm_row<F>(wimg[t >> 5][t & 31], fe_mul<F>(sc.eqw[t >> 5], p2dig<F>(t & 31)));
-  __syncthreads();
-  i32x4 wf[NW];
-#pragma unroll
-  for (int c = 0; c < NW; ++c) wf[c] = tr_frag(&wimg[c][0][0]);
-  __syncthreads();
-  ZK_TT_STAMP(trace, st, 2);
-  i32x16 acc[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[i][q] = 0;
-  const uint64_t nch = (O + 31) / 32, h8 = 8 * O;
-  uint32_t buf = 0;
-  for (uint64_t ch = blockIdx.x; ch < nch; ch += nb, buf ^= 1) {
-    const uint64_t j = ch * 32 + ql;
-    const bool valid = j < O;
-    for (int f = 0; f < 4; ++f) {  // not unrolled: one fold's inputs live at a time
-      const uint64_t e = j + (uint64_t)(2 * f + hh) * O;
-      Fe x[NW];
-#pragma unroll
-      for (int k = 0; k < NW; ++k) x[k] = valid && (uint32_t)k < nw ? ld_fe_a(X, e + k * h8) : fe_zero<F>();
-      Fe z = dm3_fold<F, NP>(x, wf);
-      if (valid) st_fe_a(X2, e, z);
-      else z = fe_zero<F>();
-      dm_row<F>(sc.img[buf][2 * f + hh][w][ql], z);
-    }
-    __syncthreads();
-    const uint32_t aX = w >> 1, aY = w & 1;
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      i32x4 fa[4], fb[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        fa[k] = tr_frag(&sc.img[buf][4 * aX + k][2 * pp][0][0]);
-        fb[k] = tr_frag(&sc.img[buf][4 * aY + k][2 * pp + 1][0][0]);
-      }
-#pragma unroll
-      for (int ux = 0; ux < 4; ++ux)
-#pragma unroll
-        for (int vy = 0; vy < 4; ++vy) {
-          const int slot = 3 * moment_digit(ux >> 1, vy >> 1) + moment_digit(ux & 1, vy & 1);
-          acc[slot] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ux], fb[vy], acc[slot], 0, 0, 0);
-        }
-    }
-  }
-  __syncthreads();
-  ZK_TT_STAMP(trace, st, 3);
-  d0t_flush(acc, sc.T);
-  __syncthreads();
-  if (t < (uint32_t)kD0TCats) diag_to_words<F>(sc.T[t], sc.w17[t]);
-  __syncthreads();
-  if (t < (uint32_t)kD0TCats) words17_to_limbs9<F>(sc.w17[t], sc.tot + t * 9);
-  __syncthreads();
-  ZK_TT_STAMP(trace, st, 4);
-  grid_finish<kD0TLimbs>(sc, sk, nb);  // drains every wave's table stores before its block counts in
-  ZK_TT_STAMP(trace, st, 5);
-  __syncthreads();                     // the scratch is reused next step
-}
-
-template <class F>
-__global__ __launch_bounds__(kBlock, 1) void k_gkr_ttail(TTailArgs a, RoundSink sink) {
-  __shared__ TTScratch sc;
-  for (uint32_t st = 0; st < a.nsteps; ++st) {
-    const uint64_t O = a.O0 >> (3 * st), nch = (O + 31) / 32;
-    const uint32_t nb = nch < gridDim.x ? (uint32_t)nch : gridDim.x;
-    if (blockIdx.x >= nb) return;  // idle from here on (nb never grows)
-    DIn din{};
-    din.ra = a.r[0];
-    din.rb = a.r[1];
-    din.rab = a.r[2];
-    din.host = a.host;
-    din.relay = a.relay + st;
-    din.err = a.err;
-    din.tag = a.rtag0 + st;
-    Fe r[3];
-    ZK_TT_STAMP(a.trace, st, 0);
-    block_get_rs(din, r[0], r[1], r[2], nb > 1);
-    ZK_TT_STAMP(a.trace, st, 1);
-    const uint32_t w = threadIdx.x >> 6;
-    const Fe* X;
-    if (st == 0) {
-      X = a.in[w];
-    } else {
-      const Fe* prev = a.out + ttail_region(a.O0, st - 1);  // 4 tables of 64 O
-      X = prev + (uint64_t)w * 64 * O;
-    }
-    Fe* X2 = a.out + ttail_region(a.O0, st) + (uint64_t)w * 8 * O;  // 4 tables of 8 O
-    RoundSink sk = sink;
-    sk.tag = sink.tag + st;
-    ttail_step<F>(sc, r, st == 0 ? a.np0 : 3u, X, X2, O, nb, sk, a.trace, st);
-  }
 }
 
 }  // namespace zk

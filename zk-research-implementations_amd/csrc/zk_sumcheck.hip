@@ -50,11 +50,10 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_DTAIL")) c->dtail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DM")) c->dm = atoi(e) != 0;
     if (const char* e = getenv("ZK_D0T")) c->d0t = atoi(e) != 0;
-    if (const char* e = getenv("ZK_D0Q")) c->d0q = atoi(e) != 0;
-    if (const char* e = getenv("ZK_TTAIL")) c->ttail = atoi(e) != 0;
     if (const char* e = getenv("ZK_DM_MIN_QUADS")) c->dm_min_quads = strtoull(e, nullptr, 0);
     if (const char* e = getenv("ZK_D0")) c->d0 = atoi(e);
     if (const char* e = getenv("ZK_CIRCUIT_DENSE")) c->circuit_dense = atoi(e) != 0;
+    if (const char* e = getenv("ZK_CIRCUIT_HOST_LGL")) c->circuit_host_lgl = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_DTAIL_MAX_QUADS")) c->dtail_max_quads = strtoull(e, nullptr, 0);
     if (const char* e = getenv("ZK_GRID_CAP")) c->grid_cap = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_ATOMIC_FANIN")) c->atomic_fanin = (uint32_t)strtoul(e, nullptr, 0);
@@ -62,6 +61,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_GATHER_VARS")) c->gather_vars = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_T33_OCT64_MIN")) c->t33_oct64_min = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_HOST_ROUNDS")) c->host_rounds = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char* e = getenv("ZK_DEVICE_FS")) c->device_fs = atoi(e) != 0;
     if (const char* e = getenv("ZK_TAIL_MAX_PAIRS")) c->tail_max_pairs = strtoull(e, nullptr, 0);
     c->num_cus = prop.multiProcessorCount;
     try {
@@ -107,14 +107,13 @@ void zk_ctx_destroy(zk_ctx* c) {
   if (c->tail_trace) (void)hipHostFree(c->tail_trace);
   if (c->block_trace) (void)hipHostFree(c->block_trace);
   c->small.release();
-  c->wide.release();
-  if (c->h_wide) (void)hipHostFree(c->h_wide);
   c->gbuf.release();
   for (auto& b : c->msm) b.release();
   for (auto& b : c->scan_tmp) b.release();
   c->g1_table.release();
   if (c->h_red) (void)hipHostFree(c->h_red);
   if (c->h_tab) (void)hipHostFree(c->h_tab);
+  if (c->h_fslog) (void)hipHostFree(c->h_fslog);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

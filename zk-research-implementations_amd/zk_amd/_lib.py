@@ -18,7 +18,7 @@ ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
 ABI_VERSION = 12  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
-KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33"]
+KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33", "coll"]
 
 
 class ZkError(RuntimeError):
@@ -37,6 +37,7 @@ class ZkStats(C.Structure):
         ("collectives", C.c_uint64),
         ("host_wait_us", C.c_double),
         ("host_work_us", C.c_double),
+        ("device_fs_rounds", C.c_uint64),
     ]
 
 

@@ -63,6 +63,7 @@ class Context:
             "host_syncs": int(s.host_syncs),
             "collectives": int(s.collectives),
             "host_wait_us": float(s.host_wait_us),
+            "device_fs_rounds": int(s.device_fs_rounds),
             "host_work_us": float(s.host_work_us),
         }
 

@@ -167,6 +167,11 @@ def _verify_kzg(proof: GkrCircuitProof, circuit: Circuit, gates, ops, coeffs, nc
 
 
 def verify(proof: GkrCircuitProof, circuit: Circuit, inputs: list[int] | None = None) -> bool:  # :128-227
+    """gkr::verify. With an input-layer KZG proof (BLS12-381 Fr) the two
+    pairing checks use proof.input_proof.g2_taus, as the reference does
+    (gkr_protocol.rs:167,175): that setup must come from a trusted source the
+    verifier holds. Taken from an untrusted prover it makes the check unsound
+    (a prover who picks its own setup can satisfy both pairings)."""
     gates, ops = circuit._abi()
     total = _rounds(gates)
     flat = [p for layer in proof.proof_polynomials for p in layer]
