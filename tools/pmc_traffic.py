@@ -98,7 +98,8 @@ def main():
     steps = []
     for (sym, alg), (name, fe), (_, wr) in zip(sched, f, w):
         assert name.startswith(sym.split("<")[0]), (name, sym)
-        steps.append({"kernel": name, "fetch_bytes": 2 * fe * 1024, "write_bytes": wr * 1024, "alg_bytes": alg})
+        steps.append({"kernel": name, "fetch_bytes": 2 * fe * 1024, "write_bytes": wr * 1024, "alg_bytes": alg,
+                      "traffic_over_alg": (2 * fe * 1024 + wr * 1024) / alg if alg else None})
 
     def summary(pred):
         rs = [r for r in steps if pred(r["kernel"])]

@@ -401,7 +401,8 @@ struct CollTimer {
     } else if (c->comm == COMM_HOST) {
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       c->stats.kernel_ms[ZK_K_COLL] += ms;
-      if (c->launch_log.size() < kLaunchLogMax) c->launch_log.push_back(zk_launch{ZK_K_COLL, ms, bytes});
+      if (((c->timing >> ZK_K_COLL) & 1u) && c->launch_log.size() < kLaunchLogMax)  // logged like a timed launch
+        c->launch_log.push_back(zk_launch{ZK_K_COLL, ms, bytes});
     }
     c->stats.launches[ZK_K_COLL] += 1;
     c->stats.alg_bytes[ZK_K_COLL] += bytes;

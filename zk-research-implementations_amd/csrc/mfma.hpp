@@ -1020,24 +1020,19 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     __syncthreads();  // the image is rewritten by the next chunk
   }
   } else {
-  if ((uint64_t)blockIdx.x < nch) {
-    in_at(blockIdx.x, 0, nx);
-    in_at(blockIdx.x, 1, nx2);
-  }
+  // (OCT 32: one fold ahead and a rolled fold loop — the small levels are
+  // latency-bound, and the unrolled loop with two folds in flight spilled 55
+  // VGPRs, whose scratch traffic was 0.4 x the kernel's bytes)
+  if ((uint64_t)blockIdx.x < nch) in_at(blockIdx.x, 0, nx);
   uint32_t buf = 0;
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x, buf ^= 1) {
-#pragma unroll
+#pragma unroll 1
     for (int f = 0; f < 4; ++f) {
       Fe x[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        x[k] = nx[k];
-        nx[k] = nx2[k];
-      }
-      if (f < 2)
-        in_at(ch, f + 2, nx2);
-      else
-        in_at(ch + gridDim.x, f - 2, nx2);  // unconditional (past the end: chunk 0, L2-resident)
+      for (int k = 0; k < 8; ++k) x[k] = nx[k];
+      // the next fold (one load site, no branch; past the end: chunk 0, L2-resident)
+      in_at(f < 3 ? ch : ch + gridDim.x, f < 3 ? f + 1 : 0, nx);
       const uint32_t corner = 2 * f + hh;
       const Fe z = dm3_fold<F>(x, wf);
       st_fold(X2, ch * 32 + ql + (uint64_t)corner * O, z);
