@@ -161,7 +161,9 @@ __device__ __forceinline__ void dfs_round(const Fe& e0, const Fe& e1, const Fe& 
       for (int j = 0; j < 4; ++j)
         s.blk[4 + 4 * lane + j] = lane < m ? ((uint64_t)cc.v[2 * j] | ((uint64_t)cc.v[2 * j + 1] << 32)) : 0;
     }
-    if (lane < 4) s.blk[lane] = (uint64_t)dig[2 * lane] | ((uint64_t)dig[2 * lane + 1] << 32);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // (static indices: a lane-indexed register array would live in scratch)
+      if (lane == (uint32_t)j) s.blk[j] = (uint64_t)dig[2 * j] | ((uint64_t)dig[2 * j + 1] << 32);
   }
   wave_sync_lds();
   uint64_t w = lane < 16 ? s.blk[lane] : 0;  // words past 4 + 4m are zero (lanes < 3 zeroed unused coefficients)
@@ -190,11 +192,40 @@ __device__ __forceinline__ void dfs_round(const Fe& e0, const Fe& e1, const Fe& 
 // 5 V20, 6 V21, 7 V12), claim = s_{m-1}(r_{m-1}), dig = d_{m-1}. Returns
 // (r_m, r_{m+1}, r_m r_{m+1}) in rr, s_{m+1}(r_{m+1}) in claim, d_{m+1} in dig;
 // lane 0 fills *log (not its tag).
+// limbs_to_fe (field.hpp) of 17 product-sum limbs, fully unrolled (registers only)
 template <class F>
-__device__ __noinline__ void dfs_double(const uint64_t* tot, Fe& claim, uint32_t (&dig)[8], Fe (&rr)[3], FsLog* log,
+__device__ __forceinline__ Fe limbs17_to_fe(const uint64_t* w) {
+  uint32_t t[24];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    const uint64_t x = (i < 17 ? w[i] : 0) + carry;
+    t[i] = (uint32_t)x;
+    carry = x >> 32;
+  }
+  Fe ch[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ch[c].v[k] = t[8 * c + k];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) ch[c] = fe_reduce_once<F>(ch[c]);  // 2^256 < 6p
+  }
+  Fe r2, one = fe_zero<F>();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r2.v[k] = F::R2[k];
+  one.v[0] = 1;
+  return fe_add<F>(fe_add<F>(fe_mul<F>(ch[0], one), ch[1]), fe_mul<F>(ch[2], r2));
+}
+
+template <class F>
+__device__ __forceinline__ void dfs_double(const uint64_t* tot, Fe& claim, uint32_t (&dig)[8], Fe (&rr)[3], FsLog* log,
                                         DfsScratch& s) {
   const uint32_t lane = threadIdx.x & 63u;
-  if (lane < 8) s.d[lane] = limbs_to_fe<F>(tot + 17 * lane, 17, true);
+  {
+    const Fe x = limbs17_to_fe<F>(tot + 17 * (lane & 7));
+    if (lane < 8) s.d[lane] = x;
+  }
   wave_sync_lds();
   Fe d[8];
 #pragma unroll

@@ -215,7 +215,7 @@ struct zk_ctx {
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
   uint32_t gather_vars = 10;  // sharded: gather the tables once <= this many local rounds remain, finish locally (ZK_GATHER_VARS; 0: at the end)
   DevBuf gbuf;                // sharded gather: fold scratch, the one-hot buffer, the interleaved global tables
-  uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN)
+  uint32_t t33_oct64_min = 4;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
   bool device_fs = false;    // the persistent tail draws its own challenges (ZK_DEVICE_FS; dfs.hpp)
@@ -237,6 +237,7 @@ struct zk_ctx {
   DevBuf msm[16];
   DevBuf scan_tmp[4];
   DevBuf g1_table;
+  DevBuf g1_table16;  // 16-bit windows (100 MB), built on the device from g1_table
 };
 
 

@@ -1183,7 +1183,11 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
           dfs_double<F>(sc.tot, claim, dig, rr, a.fslog + st, dsc);
           if (t < (uint32_t)kFsWords) {
             const uint32_t q = t & 7, g = t >> 3;
-            const uint32_t v = g == 0 ? rr[0].v[q] : g == 1 ? rr[1].v[q] : g == 2 ? rr[2].v[q] : g == 3 ? dig[q] : claim.v[q];
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)  // (static indices: lane-indexed register arrays would live in scratch)
+              if (q == (uint32_t)j)
+                v = g == 0 ? rr[0].v[j] : g == 1 ? rr[1].v[j] : g == 2 ? rr[2].v[j] : g == 3 ? dig[j] : claim.v[j];
             __hip_atomic_store(&a.relay[st + 1].w[t], ((uint64_t)(din.tag + 1) << 32) | v, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
           }

@@ -11,11 +11,10 @@ using namespace zkh;
 struct zk_kzg {
   uint32_t nv = 0;
   int device = 0;
-  std::vector<DevBuf> bases;
+  DevBuf basis;  // affine Lagrange bases of every suffix level v = 0..nv, level v at offset 2^v - 1
   std::vector<zk::G2A> g2_taus;
-  ~zk_kzg() {
-    for (auto& b : bases) b.release();
-  }
+  const zk::G1A* level(uint32_t v) const { return reinterpret_cast<const zk::G1A*>(basis.p) + (((uint64_t)1 << v) - 1); }
+  ~zk_kzg() { basis.release(); }
 };
 
 
@@ -189,6 +188,24 @@ const G1A* g1_fixed_table(zk_ctx* c) {
   return dptr<G1A>(c->g1_table);
 }
 
+// table16[w * 65536 + d] = d * 2^(16w) * G, affine on the device (built once per ctx
+// from the 8-bit table: 2^20 mixed additions and one batch normalisation)
+const G1A* g1_fixed_table16(zk_ctx* c) {
+  using namespace zk;
+  if (c->g1_table16.p) return dptr<G1A>(c->g1_table16);
+  const G1A* t8 = g1_fixed_table(c);
+  const uint64_t n = 16ull * kFB16;
+  DevBuf jac;
+  jac.ensure(n * sizeof(G1J));
+  launch(c, ZK_K_MSM, 0, 0, k_table16, grid_for(c, n, k_table16), t8, dptr<G1J>(jac));
+  c->g1_table16.ensure(n * sizeof(G1A));
+  launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
+         (const G1J*)dptr<G1J>(jac), n, dptr<G1A>(c->g1_table16));
+  sync(c);
+  jac.release();
+  return dptr<G1A>(c->g1_table16);
+}
+
 zk_g1 g1_out(const G1J& p) {
   const G1A a = zk::g1_to_affine(p);
   zk_g1 r;
@@ -269,7 +286,7 @@ void upload_fr_canonical(zk_ctx* c, zk_repr repr, const zk_fe* host, uint64_t n,
 }
 
 G1J kzg_commit_canonical(zk_ctx* c, const zk_kzg* k, uint32_t v, const Fe* scalars) {
-  return msm_g1_device(c, reinterpret_cast<const G1A*>(k->bases[v].p), scalars, (uint64_t)1 << v);
+  return msm_g1_device(c, k->level(v), scalars, (uint64_t)1 << v);
 }
 
 // KZG::get_proof (kzg.rs:59-95): quotient i of (f - v) w.r.t. its top variable,
@@ -317,9 +334,8 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
     auto k = std::make_unique<zk_kzg>();
     k->nv = nvars;
     k->device = c->device;
-    k->bases.resize(nvars + 1);
-    const uint64_t N = (uint64_t)1 << nvars;
-    const G1A* table = g1_fixed_table(c);
+    const uint64_t N = (uint64_t)1 << nvars, total = 2 * N - 1;  // every suffix level, level v at 2^v - 1
+    const G1A* table = g1_fixed_table16(c);
     DevBuf& tb = c->msm[14];
     tb.ensure(nvars * 32);
     upload<Fr381>(c, repr, taus, nvars, reinterpret_cast<Fe*>(tb.p));
@@ -327,10 +343,15 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
     sc.ensure(N * 32);
     launch(c, ZK_K_MSM, 32.0 * N, (double)N * nvars, zk::k_eq_scalars<Fr381>, grid_for(c, N, zk::k_eq_scalars<Fr381>),
            (const Fe*)tb.p, nvars, N, reinterpret_cast<Fe*>(sc.p));
-    DevBuf& jac = c->msm[13];
-    jac.ensure(N * sizeof(G1J));
-    launch(c, ZK_K_MSM, 176.0 * N, 0, zk::k_fixed_base, grid_for(c, N, zk::k_fixed_base), table,
-           (const Fe*)sc.p, N, dptr<G1J>(jac));
+    // the Jacobian points of every level (released after the normalisation)
+    struct Scoped {
+      DevBuf b;
+      ~Scoped() { b.release(); }
+    } jac;
+    jac.b.ensure(total * sizeof(G1J));
+    G1J* J = dptr<G1J>(jac.b);
+    launch(c, ZK_K_MSM, 176.0 * N, 0, zk::k_fixed_base16, grid_for(c, N, zk::k_fixed_base16), table,
+           (const Fe*)sc.p, N, J + (N - 1));
     // G2 half of run_trusted_setup (:43-46): tau_i * G2, on the host (nvars
     // scalar multiplications) while the basis kernels run
     {
@@ -342,15 +363,17 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
         k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, t));
       }
     }
-    for (uint32_t v = nvars + 1; v-- > 0;) {
+    // suffix bases L^(v)_j = L^(v+1)_j + L^(v+1)_(2^v + j) (eq sums to 1 over the
+    // dropped variable), Jacobian, then ONE batch normalisation of all levels:
+    // each normalisation launch carries a serial 381-bit inversion (~1 ms)
+    for (uint32_t v = nvars; v-- > 0;) {
       const uint64_t n = (uint64_t)1 << v;
-      if (v < nvars)
-        launch(c, ZK_K_MSM, 336.0 * n, 0, zk::k_pair_sum, grid_for(c, n, zk::k_pair_sum),
-               (const G1A*)k->bases[v + 1].p, n, dptr<G1J>(jac));
-      k->bases[v].ensure(n * sizeof(G1A));
-      launch(c, ZK_K_MSM, 240.0 * n, 0, zk::k_batch_normalize, blocks_for((n + zk::kBatchNorm - 1) / zk::kBatchNorm),
-             (const G1J*)dptr<G1J>(jac), n, dptr<G1A>(k->bases[v]));
+      launch(c, ZK_K_MSM, 432.0 * n, 0, zk::k_pair_sum, grid_for(c, n, zk::k_pair_sum), (const G1J*)(J + (2 * n - 1)),
+             n, J + (n - 1));
     }
+    k->basis.ensure(total * sizeof(G1A));
+    launch(c, ZK_K_MSM, 240.0 * total, 0, zk::k_batch_normalize, blocks_for((total + zk::kBatchNorm - 1) / zk::kBatchNorm),
+           (const G1J*)J, total, dptr<G1A>(k->basis));
     sync(c);
     *out = k.release();
   });
@@ -369,7 +392,7 @@ int zk_kzg_lagrange_basis(zk_ctx* c, const zk_kzg* k, uint32_t nvars_suffix, zk_
     bind(c);
     const uint64_t n = (uint64_t)1 << nvars_suffix;
     std::vector<G1A> a(n);
-    HIPCK(hipMemcpyAsync(a.data(), k->bases[nvars_suffix].p, n * sizeof(G1A), hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipMemcpyAsync(a.data(), k->level(nvars_suffix), n * sizeof(G1A), hipMemcpyDeviceToHost, c->stream));
     sync(c);
     for (uint64_t i = 0; i < n; ++i) out[i] = g1a_out(a[i]);
   });

@@ -150,16 +150,27 @@ __global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict_
 }
 
 // ---- fixed-base scalar multiplication (Lagrange basis setup) ----------------------
-// table[w * 256 + d] = d * 2^(8w) * G (affine); out[i] = scalars[i] * G
-__global__ __launch_bounds__(kBlock) void k_fixed_base(const G1A* __restrict__ table, const Fe* __restrict__ scalars,
-                                                       uint64_t n, G1J* __restrict__ out) {
+// 16-bit windows: table16[w * 65536 + d] = d * 2^(16w) * G (affine), built on
+// the device from the 8-bit table (one mixed addition per entry, then one
+// batch normalisation); out[i] = scalars[i] * G with 16 mixed additions per
+// point instead of 32 (the lookups stream from a 100 MB table)
+constexpr uint32_t kFB16 = 65536;
+__global__ __launch_bounds__(kBlock) void k_table16(const G1A* __restrict__ t8, G1J* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < 16ull * kFB16; i += stride) {
+    const uint32_t w = (uint32_t)(i >> 16), d = (uint32_t)i & 0xffffu;
+    out[i] = g1_add_mixed(g1_from_affine(t8[(2 * w) * 256 + (d & 0xffu)]), t8[(2 * w + 1) * 256 + (d >> 8)]);
+  }
+}
+__global__ __launch_bounds__(kBlock) void k_fixed_base16(const G1A* __restrict__ table, const Fe* __restrict__ scalars,
+                                                         uint64_t n, G1J* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     const Fe s = ld_fe(scalars, i);
     G1J acc = g1_inf();
-    for (uint32_t w = 0; w < 32; ++w) {
-      const uint32_t d = (s.v[w >> 2] >> ((w & 3) * 8)) & 0xffu;
-      if (d) acc = g1_add_mixed(acc, table[w * 256 + d]);
+    for (uint32_t w = 0; w < 16; ++w) {
+      const uint32_t d = (s.v[w >> 1] >> ((w & 1) * 16)) & 0xffffu;
+      if (d) acc = g1_add_mixed(acc, table[(uint64_t)w * kFB16 + d]);
     }
     out[i] = acc;
   }
@@ -184,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void k_eq_scalars(const Fe* __restrict__ ta
 // Jacobian -> affine, kBatchNorm points per thread sharing one inversion
 // (Montgomery's trick); the prefix products are parked in out[].x until the
 // backward pass overwrites them; infinity stays (0, 0)
-constexpr uint32_t kBatchNorm = 32;
+constexpr uint32_t kBatchNorm = 64;
 __global__ __launch_bounds__(kBlock) void k_batch_normalize(const G1J* __restrict__ in, uint64_t n,
                                                             G1A* __restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -210,11 +221,12 @@ __global__ __launch_bounds__(kBlock) void k_batch_normalize(const G1J* __restric
   }
 }
 
-// suffix basis: out[j] = in[j] + in[j + half] (Jacobian; normalised afterwards)
-__global__ __launch_bounds__(kBlock) void k_pair_sum(const G1A* __restrict__ in, uint64_t half, G1J* __restrict__ out) {
+// suffix basis: out[j] = in[j] + in[j + half], Jacobian in and out (every
+// level is normalised afterwards in one batch)
+__global__ __launch_bounds__(kBlock) void k_pair_sum(const G1J* __restrict__ in, uint64_t half, G1J* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < half; j += stride)
-    out[j] = g1_add_mixed(g1_from_affine(in[j]), in[j + half]);
+    out[j] = g1_add(in[j], in[j + half]);
 }
 
 // KZG quotient of the top variable: q[j] = f[j + half] - f[j] (get_quotient, kzg.rs:150-161)
