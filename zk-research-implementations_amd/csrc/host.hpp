@@ -244,7 +244,7 @@ struct zk_ctx {
 namespace zkh {
 // small device area: [0,2048) round sums (<= 256 u64), [2048] input check
 // flag, [2560,3712) fan-in counters (9 x 128 B), [4096,6144) limb accumulator
-// (<= 256 u64), [6144,6656) single-round relay slots (8 x 64 B), [6656,6912)
+// (<= 256 u64), [6144,6656) single-round relay slots (8 x 64 B), [6656,7168)
 // the double-round relay slot, [8192, +64 KiB) all-reduce bounce buffer
 // (<= 256 ranks x 256 B), then the tail's 4 local elements and the gathered
 // 4 x world tables
@@ -265,6 +265,7 @@ inline uint32_t* h_err(zk_ctx* c) { return reinterpret_cast<uint32_t*>(reinterpr
 inline zk::RPost* h_rpost(zk_ctx* c) { return reinterpret_cast<zk::RPost*>(reinterpret_cast<char*>(c->h_red) + 6144); }
 inline zk::RWait* d_relay(zk_ctx* c) { return reinterpret_cast<zk::RWait*>(reinterpret_cast<char*>(c->small.p) + 6144); }
 inline zk::RPost* d_rpost(zk_ctx* c) { return reinterpret_cast<zk::RPost*>(reinterpret_cast<char*>(c->small.p) + 6656); }
+static_assert(6656 + sizeof(zk::RPost) <= 8192 && 6144 + sizeof(zk::RPost) <= kHostPage, "relay slot overlaps");
 
 inline void bind(zk_ctx* c) { HIPCK(hipSetDevice(c->device)); }
 
@@ -582,6 +583,14 @@ struct PostR {
       __atomic_store_n(&s->w[16 + i], t | rab.v[i], __ATOMIC_RELAXED);
     }
   }
+  // a fold by three (k_gkr_t33, k_gkr_dm3): the eight eq weights (kernels.hpp block_get_eq8)
+  void post8(const Fe (&e)[8], uint32_t tag) {
+    note();
+    zk::RPost* s = h_rpost(c);
+    const uint64_t t = (uint64_t)tag << 32;
+    for (int k = 0; k < 8; ++k)
+      for (int i = 0; i < 8; ++i) __atomic_store_n(&s->w[8 * k + i], t | e[k].v[i], __ATOMIC_RELAXED);
+  }
   // the device-FS tail's first step: also the transcript digest and the claim (dfs.hpp kFsWords)
   void post5(const Fe& ra, const Fe& rb, const Fe& rab, const uint32_t (&dig)[8], const Fe& claim, uint32_t tag) {
     zk::RPost* s = h_rpost(c);
@@ -595,7 +604,9 @@ struct PostR {
   ~PostR() {
     if (done || last == 0) return;
     post(zk::fe_zero<zk::Bn254Fr>(), last);
-    post2(zk::fe_zero<zk::Bn254Fr>(), zk::fe_zero<zk::Bn254Fr>(), zk::fe_zero<zk::Bn254Fr>(), last);
+    Fe z[8];
+    for (auto& x : z) x = zk::fe_zero<zk::Bn254Fr>();
+    post8(z, last);  // every word of the slot (any step's reader)
     (void)hipStreamSynchronize(c->stream);
   }
 };
@@ -1068,7 +1079,16 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     const GStep& nx = steps[si + 1];
     if (nx.kind == GS_HOST) return;
     if (nx.kind == GS_T32 || nx.kind == GS_T33) {
-      post.post2(rz, ra, rb, rtags[si + 1]);
+      // eq((rz, ra, rb), c), c = 4a + 2b + c0 (rz, the oldest, on the top bit): the
+      // fold's eight weights, formed here instead of in every block of the step
+      const Fe one = zk::fe_one<F>();
+      Fe e[8];
+      for (int q = 0; q < 8; ++q) {
+        const Fe fa = (q & 4) ? rz : zk::hfe_sub<F>(one, rz), fb = (q & 2) ? ra : zk::hfe_sub<F>(one, ra);
+        const Fe fc = (q & 1) ? rb : zk::hfe_sub<F>(one, rb);
+        e[q] = zk::hfe_mul<F>(zk::hfe_mul<F>(fa, fb), fc);
+      }
+      post.post8(e, rtags[si + 1]);
     } else if (nx.kind == GS_DTAIL && nx.dfs) {
       // the sponge after a challenge is the zero state + its 32-byte digest
       // buffered (dfs.hpp): the device continues the transcript from there

@@ -845,7 +845,9 @@ __global__ __launch_bounds__(kBlock) void k_gkr_tail(TailArgs a, RoundSink sink)
 // between the words is needed.
 // ---------------------------------------------------------------------------
 struct alignas(64) RPost {
-  uint64_t w[40];  // ra, rb, rab in words 0-23; the device-FS tail also the digest (24-31) and the claim (32-39)
+  // ra, rb, rab in words 0-23 (the device-FS tail also the digest, 24-31, and
+  // the claim, 32-39); a fold by three reads the eight eq weights, words 0-63
+  uint64_t w[64];
 };
 struct DIn {
   Fe ra, rb, rab;      // used as is when host == null
@@ -896,6 +898,30 @@ __device__ __forceinline__ void block_get_rs(const DIn& in, Fe& ra, Fe& rb, Fe& 
     ra.v[i] = s_w[i];
     rb.v[i] = s_w[8 + i];
     rab.v[i] = s_w[16 + i];
+  }
+}
+
+// The eight eq weights eq((ra, rb, rc), c), c = 4a + 2b + c0, of a fold by the
+// three pending challenges (k_gkr_t33, k_gkr_dm3) into eqw[0..7] (LDS; valid
+// after the caller's next barrier): a pre-enqueued step reads them as posted by
+// the host (64 tagged words: two dependent Montgomery products per weight off
+// the step's critical path), a step launched after its challenges forms them
+// from din's (ra, rb, rab = rc).
+template <class F>
+__device__ __forceinline__ void block_get_eq8(const DIn& in, Fe* eqw, bool relay) {
+  const uint32_t t = threadIdx.x;
+  if (in.host) {
+    __shared__ uint32_t s_w[64];
+    block_get_words<8>(in, s_w, relay, false);
+    if (t < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) eqw[t].v[i] = s_w[8 * t + i];
+    }
+  } else if (t < 8) {
+    const Fe one = fe_one<F>();
+    const Fe fa = (t & 4) ? in.ra : fe_sub<F>(one, in.ra), fb = (t & 2) ? in.rb : fe_sub<F>(one, in.rb);
+    const Fe fc = (t & 1) ? in.rab : fe_sub<F>(one, in.rab);
+    eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
   }
 }
 

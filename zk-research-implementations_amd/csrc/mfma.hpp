@@ -805,18 +805,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm3(const Fe* __restrict__ A,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
                                                       Fe* __restrict__ P2, uint64_t Q, DIn din, RoundSink sink) {
-  Fe ra, rb, rc;
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
-  block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc (not ra rb) for this step
-  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   __shared__ DM3Scratch sc;
+  block_get_eq8<F>(din, sc.eqw, gridDim.x > 1);  // eq((ra, rb, rc), c), c = 4a + 2b + c0
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63;
-  if (t < 8) {  // eq((ra, rb, rc), c), c = 4a + 2b + c0
-    const Fe one = fe_one<F>();
-    const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
-    const Fe fc = (t & 1) ? rc : fe_sub<F>(one, rc);
-    sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
-  }
   for (uint32_t i = t; i < kDCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
   __syncthreads();
   // the constants' digit rows borrow the product image until their fragments are in registers
@@ -901,7 +894,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
                                                       Fe* __restrict__ P2, uint64_t O, DIn din, RoundSink sink) {
   constexpr int NI = 8;  // inputs per output
-  Fe ra, rb, rc;
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
   const Fe* __restrict__ X = uniform_ptr(w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P)));
@@ -922,10 +914,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
 #pragma unroll
     for (int k = 0; k < NI; ++k) x[k] = ld_fe(X, e + k * h8);
   };
-  // Inputs two folds ahead (one wave per SIMD: the loads in flight are what
-  // hides HBM latency). OCT 64: the first two units (written by
-  // the previous kernel) are in flight while the host posts the challenges
-  // (OCT 32 loads them after the constants: held across them it spills).
+  // Inputs two folds ahead for OCT 64, one for OCT 32 (one wave per SIMD: the
+  // loads in flight are what hides HBM latency). The first ones (written by
+  // the previous kernel) are in flight while the host posts the challenges.
   // Block 0's wave 0 polls the host for the challenges and relays them to
   // every block: its poll would wait behind these loads (vmcnt is in order),
   // so it loads after the challenges arrive.
@@ -936,24 +927,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
   };
   Fe nx[8], nx2[8];
-  const bool early = OCT == 64 && (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
-  if (early) {
-    unit_at(blockIdx.x, 0, nx);
-    unit_at(blockIdx.x, 1, nx2);
-  }
-  block_get_rs(din, ra, rb, rc, gridDim.x > 1);  // the third word group carries rc for this step
-  if (OCT == 64 && !early && (uint64_t)blockIdx.x < nch) {
-    unit_at(blockIdx.x, 0, nx);
-    unit_at(blockIdx.x, 1, nx2);
-  }
-  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
+  const bool early = (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
+  auto first_loads = [&]() {
+    if constexpr (OCT == 64) {
+      unit_at(blockIdx.x, 0, nx);
+      unit_at(blockIdx.x, 1, nx2);
+    } else {
+      in_at(blockIdx.x, 0, nx);
+    }
+  };
+  if (early) first_loads();
   __shared__ T33Scratch sc;
-  if (t < (uint32_t)NI) {  // eq(r, c), the oldest pending challenge on c's top bit: c = 4a + 2b + c0
-    const Fe one = fe_one<F>();
-    const Fe fa = (t & 4) ? ra : fe_sub<F>(one, ra), fb = (t & 2) ? rb : fe_sub<F>(one, rb);
-    const Fe fc = (t & 1) ? rc : fe_sub<F>(one, rc);
-    sc.eqw[t] = fe_mul<F>(fe_mul<F>(fa, fb), fc);
-  }
+  block_get_eq8<F>(din, sc.eqw, gridDim.x > 1);  // eq(r, c), the oldest pending challenge on c's top bit
+  if (!early && (uint64_t)blockIdx.x < nch) first_loads();
+  if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
   for (uint32_t i = t; i < kD0TCats * 64; i += kBlock) (&sc.T[0][0])[i] = 0;
   stage_p2w<F>(sc.p2w);
   __syncthreads();
@@ -1023,7 +1010,6 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   // (OCT 32: one fold ahead and a rolled fold loop — the small levels are
   // latency-bound, and the unrolled loop with two folds in flight spilled 55
   // VGPRs, whose scratch traffic was 0.4 x the kernel's bytes)
-  if ((uint64_t)blockIdx.x < nch) in_at(blockIdx.x, 0, nx);
   uint32_t buf = 0;
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x, buf ^= 1) {
 #pragma unroll 1
