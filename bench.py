@@ -339,7 +339,7 @@ def e2e_bench(ctx, field: int, tabs, n: int, reps: int = 3) -> dict:
     }
 
 
-def circuit_bench(ctx, field: int, log_inputs: int = 12, reps: int = 3) -> dict:
+def circuit_bench(ctx, field: int, log_inputs: int = 12, reps: int = 7) -> dict:
     """a full GKR prove over a random binary-tree circuit with
     2^log_inputs inputs — circuit evaluation, every layer's two-phase sum-check
     over tables of 2G entries (sparse wiring) on the device, transcript on the
@@ -356,24 +356,35 @@ def circuit_bench(ctx, field: int, log_inputs: int = 12, reps: int = 3) -> dict:
     p = zk_amd.modulus(field)
     inputs = [rng.randrange(p) for _ in range(1 << log_inputs)]
     circ = Circuit(structure, field)
-    proof = prove(circ, inputs, ctx)  # warm-up
-    ok = verify(proof, circ, inputs)
-    ctx.reset_stats()
-    ctx.set_timing_kinds(["layer"])
-    times = []
-    for _ in range(reps):
+    from zk_amd.elems import as_limbs
+
+    x = as_limbs(inputs)  # the C ABI's element layout (uint64[n, 4]), as a Rust caller holds Vec<Fr>
+    proof = prove(circ, x, ctx)  # warm-up
+    ok = verify(proof, circ, inputs) and prove(circ, inputs, ctx).random_challenges == proof.random_challenges
+    times, times_int = [], []
+    for _ in range(reps):  # wall time of the API call, no events
         t0 = time.perf_counter()
-        prove(circ, inputs, ctx)
+        prove(circ, x, ctx)
         times.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        prove(circ, inputs, ctx)  # the same with Python-int inputs (adds their conversion)
+        times_int.append(time.perf_counter() - t0)
+    ctx.reset_stats()  # one more proof with HIP events on the layer kernels
+    ctx.set_timing_kinds(["layer"])
+    prove(circ, inputs, ctx)
     ctx.set_timing(False)
     k = ctx.stats()["kernels"]["layer"]
     times.sort()
+    times_int.sort()
     return {
         "workload": f"gkr::prove over a random {log_inputs}-layer binary-tree circuit, {1 << log_inputs} inputs "
                     f"(input-layer sum-check over {2 * log_inputs} variables), {'BN254 Fr' if field == 0 else field}",
         "ms_median": times[len(times) // 2] * 1e3,
+        "inputs": "uint64[n, 4] limb array (the C ABI layout)",
+        "ms_median_python_int_inputs": times_int[len(times_int) // 2] * 1e3,
         "verified": ok,
-        "layer_kernels_ms_per_proof": k["ms"] / reps,
+        "reps": reps,
+        "layer_kernels_ms_per_proof": k["ms"],
         "layer_prover": "dense (2G)^2 tables" if os.environ.get("ZK_CIRCUIT_DENSE", "0") not in ("", "0")
         else "two phases over tables of 2G entries",
         "note": "the reference builds add_i/mul_i densely (2^(3g+2) entries: 2^35 at this size) and cannot run it",
@@ -659,12 +670,12 @@ def main() -> None:
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
 
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "r3_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "r4_traffic.json")
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
         if t.get("kind") == dom and field == 0:  # the longest launch of this workload
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
-            traffic_src = f"profiles/r3_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.3f}"
+            traffic_src = f"profiles/r4_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.4f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
     if rank == 0:
         out = {

@@ -27,8 +27,9 @@ def _circuit(rng: random.Random, depth: int, out_gates: int) -> list[list[str]]:
                                                    (2, 2, 2), (0, 5, 2)])
 def test_device_proof_equals_oracle(monkeypatch, field, depth, out_gates, host_lgl):
     """ZK_CIRCUIT_HOST_LGL: layers with tables of <= 2^this entries run on the
-    host (8, the default: these circuits entirely), none (0: every layer on the
-    device), or the top ones (3). Every split gives the oracle's proof."""
+    host (8; the default 9 also runs these circuits entirely there), none (0:
+    every layer on the device), or the top ones (3). Every split gives the
+    oracle's proof."""
     import zk_amd
 
     monkeypatch.setenv("ZK_CIRCUIT_HOST_LGL", host_lgl)
@@ -71,7 +72,9 @@ def test_two_phase_equals_dense_tables(monkeypatch, field):
     ZK_CIRCUIT_DENSE=1 (the four L^2 tables, then the generic sum-check) give
     the same proof on a 2^10-input circuit (input layer: 20 sum-check rounds);
     so do every layer on the device (ZK_CIRCUIT_HOST_LGL=0) and every layer on
-    the host (10)."""
+    the host (10). On the device, layers of 2^9 and 2^10 entries end their
+    phases in host rounds (2 and 4 of them) and take w(r_b), w(r_c) from the
+    folded tables; the dense route evaluates w on the device (k_mle_eval2)."""
     import zk_amd
 
     rng = random.Random(5 + field)

@@ -60,11 +60,16 @@ struct CircuitOut {
 // entries (kernels.hpp k_phase1_tables / k_phase2_tables): the same round
 // polynomials and challenges as gkr_prove over the dense L^2 tables, since
 // every round value is the same field sum. Phase 1 binds b (rounds 0 .. lgL-1),
-// w(r_b) is evaluated on the device, phase 2 binds c; both phases run the
-// device sum-check of the hot path (gkr_phase) on the shared transcript.
+// phase 2 binds c; both phases run the device sum-check of the hot path
+// (gkr_phase) on the shared transcript, their last rounds on the host.
+// The layer's two evaluations come out of the folds: phase 1's W = w folded by
+// r_b is w(r_b), and phase 2's S(c) = w(r_b) + w(c) folded by r_c is
+// w(r_b) + w(r_c) (a multilinear extension plus a constant), so ev = {w(r_b),
+// w(r_c)} (gkr_protocol.rs:75-76) without another pass over w — when a phase
+// ends on the host (FinalVals); otherwise k_mle_eval2 evaluates w.
 template <class F>
 void gkr_layer_two_phase(zk_ctx* c, const Fe* w, const Fe* wt, const uint8_t* ops, uint32_t lgL, zk_transcript* tr,
-                         GkrOut& out) {
+                         GkrOut& out, Fe (&ev)[2]) {
   const uint32_t nv = 2 * lgL;
   const uint64_t L = (uint64_t)1 << lgL;
   out.coeffs.assign(3 * (size_t)nv, zk::fe_zero<F>());
@@ -83,17 +88,34 @@ void gkr_layer_two_phase(zk_ctx* c, const Fe* w, const Fe* wt, const uint8_t* op
   const Fe* cur[4] = {t1, t1 + L, t1 + 2 * L, t1 + 3 * L};
   Fe claim = zk::fe_zero<F>(), r = zk::fe_zero<F>();
   uint32_t pend = 0;
-  gkr_phase<F>(c, cur, lgL, 0, false, tr, out, claim, r, pend);  // rounds 0 .. lgL-1 (b)
-  zk::LayerPts ep{};  // w(r_b) in both slots of the two-point evaluation
+  FinalVals f1, f2;
+  gkr_phase<F>(c, cur, lgL, 0, false, tr, out, claim, r, pend, true, 0, nullptr, &f1);  // rounds 0 .. lgL-1 (b)
+  zk::LayerPts ep{};  // r_b, then r_c once phase 2 has drawn it
   for (uint32_t k = 0; k < lgL; ++k) ep.r[k] = ep.r[lgL + k] = out.challenges[k];
-  const zk::RoundSink sk = make_sink(c, false);
-  launch(c, ZK_K_LAYER, 32.0 * L, 4.0 * L, zk::k_mle_eval2<F>, grid_for(c, L, zk::k_mle_eval2<F>), w, lgL, ep, sk);
-  Fe ev[2];
-  collect_sums<F, 2>(c, sk, false, 17, ev);
+  auto eval2 = [&](Fe (&v)[2]) {  // w at ep.r[0..lgL) and ep.r[lgL..2 lgL) on the device
+    const zk::RoundSink sk = make_sink(c, false);
+    launch(c, ZK_K_LAYER, 32.0 * L, 4.0 * L, zk::k_mle_eval2<F>, grid_for(c, L, zk::k_mle_eval2<F>), w, lgL, ep, sk);
+    collect_sums<F, 2>(c, sk, false, 17, v);
+  };
+  if (f1.ok) {
+    ev[0] = f1.v[0];
+  } else {
+    Fe v[2];
+    eval2(v);
+    ev[0] = v[0];
+  }
   launch(c, ZK_K_LAYER, 160.0 * L, (double)L * (lgL + 2), zk::k_phase2_tables<F>, blocks, w, wt, ops, lgL, ep, ev[0],
          t2, t2 + L, t2 + 2 * L, t2 + 3 * L);
   const Fe* cur2[4] = {t2, t2 + L, t2 + 2 * L, t2 + 3 * L};
-  gkr_phase<F>(c, cur2, lgL, lgL, false, tr, out, claim, r, pend);  // rounds lgL .. 2 lgL-1 (c)
+  gkr_phase<F>(c, cur2, lgL, lgL, false, tr, out, claim, r, pend, true, 0, nullptr, &f2);  // rounds lgL .. 2 lgL-1 (c)
+  if (f2.ok) {
+    ev[1] = zk::hfe_sub<F>(f2.v[1], ev[0]);
+  } else {
+    for (uint32_t k = 0; k < lgL; ++k) ep.r[lgL + k] = out.challenges[lgL + k];
+    Fe v[2];
+    eval2(v);
+    ev[1] = v[1];
+  }
   sync(c);
 }
 
@@ -124,31 +146,30 @@ void host_layer_phase(std::vector<Fe> (&T)[4], uint32_t n, uint32_t k0, zk_trans
       h64::mac_wide(a2, x2[2], x2[3]);
     }
     finish_round<F>(tr, wide_to_fe<F>(a0), wide_to_fe<F>(a1), wide_to_fe<F>(a2), k0 + i, out, r);
-    if (i + 1 < n) host_fold<F>(T, r);
+    host_fold<F>(T, r);  // (after the last round: the tables at the phase's point, one entry each)
   }
 }
+// eq(pt, v) for every v < 2^n, bit n-1-k of v against pt[k] (MSB first):
+// one product per entry (the table doubles once per coordinate)
 template <class F>
-Fe host_mle_eval(const Fe* w, uint32_t n, const Fe* pt) {  // MultilinearPoly::evaluate (:79-91)
-  std::vector<Fe> t(w, w + ((size_t)1 << n));
+std::vector<Fe> host_eq_table(const Fe* pt, uint32_t n) {
+  std::vector<Fe> t(1, zk::fe_one<F>());
   for (uint32_t k = 0; k < n; ++k) {
-    const size_t h = t.size() / 2;
-    for (size_t j = 0; j < h; ++j) t[j] = zk::hfe_add<F>(t[j], zk::hfe_mul<F>(pt[k], zk::hfe_sub<F>(t[j + h], t[j])));
-    t.resize(h);
+    std::vector<Fe> u(2 * t.size());
+    for (size_t j = 0; j < t.size(); ++j) {
+      const Fe x = zk::hfe_mul<F>(t[j], pt[k]);
+      u[2 * j] = zk::hfe_sub<F>(t[j], x);
+      u[2 * j + 1] = x;
+    }
+    t.swap(u);
   }
-  return t[0];
-}
-// eq(pt, v) over n bits, MSB first
-template <class F>
-Fe host_eq(const Fe* pt, uint64_t v, uint32_t n) {
-  Fe e = zk::fe_one<F>();
-  for (uint32_t k = 0; k < n; ++k)
-    e = zk::hfe_mul<F>(e, ((v >> (n - 1 - k)) & 1u) ? pt[k] : zk::hfe_sub<F>(zk::fe_one<F>(), pt[k]));
-  return e;
+  return t;
 }
 // w = the layer's L inputs, wt = its G gate weights (k_gate_weights), ops its gate ops
+// (ev = {w(r_b), w(r_c)} from the folds, as in gkr_layer_two_phase)
 template <class F>
 void host_layer(const Fe* w, const std::vector<Fe>& wt, const uint8_t* ops, uint32_t lgL, zk_transcript* tr,
-                GkrOut& out) {
+                GkrOut& out, Fe (&ev)[2]) {
   using namespace zk;
   const uint32_t nv = 2 * lgL;
   const size_t L = (size_t)1 << lgL;
@@ -172,18 +193,21 @@ void host_layer(const Fe* w, const std::vector<Fe>& wt, const uint8_t* ops, uint
   }
   host_layer_phase<F>(T, lgL, 0, tr, out);
   const Fe* rb = out.challenges.data();
-  const Fe wrb = host_mle_eval<F>(w, lgL, rb);
+  const Fe wrb = T[0][0];  // W = w folded by r_b
   for (auto& t : T) t.assign(L, fe_zero<F>());  // phase 2 (k_phase2_tables): A, S, M, P over c
+  const std::vector<Fe> eqb = host_eq_table<F>(rb, lgL);
   for (size_t cc = 0; cc < L; ++cc) {
     if (cc & 1) {
       const size_t b = cc - 1;
-      const Fe e = hfe_mul<F>(wt[b >> 1], host_eq<F>(rb, b, lgL));
+      const Fe e = hfe_mul<F>(wt[b >> 1], eqb[b]);
       (ops[b >> 1] ? T[2] : T[0])[cc] = e;
     }
     T[1][cc] = hfe_add<F>(wrb, w[cc]);
     T[3][cc] = hfe_mul<F>(wrb, w[cc]);
   }
   host_layer_phase<F>(T, lgL, lgL, tr, out);
+  ev[0] = wrb;
+  ev[1] = hfe_sub<F>(T[1][0], wrb);  // S = w(r_b) + w(c) folded by r_c
 }
 
 template <class F>
@@ -278,20 +302,23 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     }
     GkrOut g;
     const bool on_host = lgL <= host_lgl && off[l] >= hbase;
-    Fe o1, o2;
+    Fe o1, o2, lev[2];
+    bool have_ev = false;
     if (on_host) {  // gate weights, both phases and both evaluations on the host
       if (dbg) t1 = clk::now();
       std::vector<Fe> wt(G);
+      const std::vector<Fe> eb = host_eq_table<F>(pts.data(), W);
+      const std::vector<Fe> ec = has_c ? host_eq_table<F>(pts.data() + W, W) : std::vector<Fe>();
       for (uint32_t gi = 0; gi < G; ++gi) {  // k_gate_weights
-        Fe wg = hfe_mul<F>(a, host_eq<F>(pts.data(), gi, W));
-        if (has_c) wg = hfe_add<F>(wg, hfe_mul<F>(b, host_eq<F>(pts.data() + W, gi, W)));
+        Fe wg = hfe_mul<F>(a, eb[gi]);
+        if (has_c) wg = hfe_add<F>(wg, hfe_mul<F>(b, ec[gi]));
         wt[gi] = wg;
       }
       const Fe* hw = hvals.data() + (off[l] - hbase);
-      host_layer<F>(hw, wt, ops + opoff[l], lgL, &tr, g);
+      host_layer<F>(hw, wt, ops + opoff[l], lgL, &tr, g, lev);
       if (dbg) t2 = clk::now();
-      o1 = host_mle_eval<F>(hw, lgL, g.challenges.data());
-      o2 = host_mle_eval<F>(hw, lgL, g.challenges.data() + lgL);
+      o1 = lev[0];
+      o2 = lev[1];
     }
     LayerPts lp{};
     std::copy(pts.begin(), pts.end(), lp.r);
@@ -313,7 +340,8 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
       gkr_prove_device<F>(c, dT, nv, false, &tr, g);  // gkr_prove(claimed_sum, &fbc_poly, &mut transcript) (:68)
     } else {  // two phases over tables of size L (kernels.hpp k_phase1_tables / k_phase2_tables)
       if (dbg) t1 = clk::now();
-      gkr_layer_two_phase<F>(c, w, dwt.b.fe(0), dop + opoff[l], lgL, &tr, g);
+      gkr_layer_two_phase<F>(c, w, dwt.b.fe(0), dop + opoff[l], lgL, &tr, g, lev);
+      have_ev = true;
     }
     if (dbg) t2 = clk::now();
     for (uint32_t k = 0; k < nv; ++k) {
@@ -324,7 +352,10 @@ void gkr_circuit_prove_device(zk_ctx* c, zk_repr repr, uint32_t nlayers, const u
     k0 += nv;
     rb.assign(g.challenges.begin(), g.challenges.begin() + nv / 2);  // (:71-73)
     rc.assign(g.challenges.begin() + nv / 2, g.challenges.end());
-    if (!on_host) {  // o1 = w.evaluate(r_b), o2 = w.evaluate(r_c) (:75-76): one fused pass
+    if (have_ev) {  // the two-phase prover's folds (gkr_layer_two_phase)
+      o1 = lev[0];
+      o2 = lev[1];
+    } else if (!on_host) {  // o1 = w.evaluate(r_b), o2 = w.evaluate(r_c) (:75-76): one fused pass
       LayerPts ep{};
       std::copy(rb.begin(), rb.end(), ep.r);
       std::copy(rc.begin(), rc.end(), ep.r + lgL);

@@ -223,7 +223,7 @@ struct zk_ctx {
   size_t h_tab_bytes = 0;
   bool tail = true;         // (ZK_DROUND=0 only) pre-enqueued small rounds in one persistent kernel (ZK_TAIL=0: one launch each)
   bool circuit_dense = false;  // circuit GKR: dense L^2 layer tables instead of the two-phase prover (ZK_CIRCUIT_DENSE)
-  uint32_t circuit_host_lgl = 8;  // circuit GKR: layers with tables of <= 2^this entries run on the host (ZK_CIRCUIT_HOST_LGL)
+  uint32_t circuit_host_lgl = 9;  // circuit GKR: layers with tables of <= 2^this entries run on the host (ZK_CIRCUIT_HOST_LGL)
   uint64_t tail_max_pairs = 1u << 15;  // the tail starts at the first round with <= this many pairs (ZK_TAIL_MAX_PAIRS)
   uint64_t* tail_trace = nullptr;      // ZK_DEBUG_TAIL: pinned per-round stamps of the tail kernel, printed per proof
   uint64_t* block_trace = nullptr;     // ZK_DEBUG_BLOCKS=<step>: pinned per-block stamps of that step (needs ZK_DEBUG_TAIL)
@@ -374,7 +374,7 @@ inline bool multi_rank(zk_ctx* c) { return (c->world > 1 || c->force_coll) && c-
 // Collective timing (ZK_K_COLL): an RCCL collective on the stream is bracketed
 // by events when that kind is timed (its duration then joins the launch log
 // like a kernel's); a host communicator's callback is host wall time, counted
-// always. `bytes` = what this rank sends.
+// under the same condition. `bytes` = what this rank sends.
 struct CollTimer {
   zk_ctx* c;
   double bytes;
@@ -400,11 +400,10 @@ struct CollTimer {
     if (p.a) {
       (void)hipEventRecord(p.b, c->stream);
       c->pending.push_back(p);
-    } else if (c->comm == COMM_HOST) {
+    } else if (c->comm == COMM_HOST && ((c->timing >> ZK_K_COLL) & 1u)) {  // timed like a kernel kind
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       c->stats.kernel_ms[ZK_K_COLL] += ms;
-      if (((c->timing >> ZK_K_COLL) & 1u) && c->launch_log.size() < kLaunchLogMax)  // logged like a timed launch
-        c->launch_log.push_back(zk_launch{ZK_K_COLL, ms, bytes});
+      if (c->launch_log.size() < kLaunchLogMax) c->launch_log.push_back(zk_launch{ZK_K_COLL, ms, bytes});
     }
     c->stats.launches[ZK_K_COLL] += 1;
     c->stats.alg_bytes[ZK_K_COLL] += bytes;
@@ -696,12 +695,22 @@ void host_round_sums(const std::vector<Fe> (&T)[4], Fe& e0, Fe& e2) {
   e2 = wide_to_fe<F>(a2);
 }
 
+// The four tables folded by every challenge of a phase (the multilinear
+// extensions at the phase's point), when its last rounds ran on the host.
+struct FinalVals {
+  Fe v[4];
+  bool ok = false;
+};
+
 // gather_max > 0 (sharded phases): stop after the first step boundary b with
 // nv - b <= gather_max; *stop = b (nv when the phase runs to its end).
+// fin: filled (fin->ok) when the phase ends in host rounds — one more host
+// fold of the last two entries by the last challenge.
 template <class F>
 void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool across_ranks, zk_transcript* tr,
                GkrOut& out, Fe& claim, Fe& r, uint32_t& pend, bool host_ok = false, uint32_t gather_max = 0,
-               uint32_t* stop = nullptr) {
+               uint32_t* stop = nullptr, FinalVals* fin = nullptr) {
+  if (fin) fin->ok = false;
   const uint64_t L = (uint64_t)1 << nv;
   const bool pre = prelaunch(c, nv);
   std::vector<GStep> steps;
@@ -740,21 +749,24 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     for (; i + 1 < nv; i += 2, np = 2) steps.push_back({GS_DOUBLE, i, np});
     // host rounds: the last H rounds, if they are whole double steps and the
     // persistent tail keeps >= 2 device steps before them
+    // (H = ZK_HOST_ROUNDS, or fewer when that leaves the tail < 2 steps: odd
+    // round counts at n = 9, 11 take H = 2)
     uint32_t hostH = 0;
     if (host_ok && pre && c->dtail && use_tail(c, across_ranks) && !(across_ranks && multi_rank(c)) && c->host_rounds >= 2) {
-      const uint32_t H = c->host_rounds & ~1u;
-      size_t k = steps.size();
-      uint32_t got = 0;
-      while (got < H && k > 0 && steps[k - 1].kind == GS_DOUBLE && steps[k - 1].np == 2) {
-        --k;
-        got += 2;
-      }
-      size_t smalls = 0;  // device double steps left for the persistent tail
-      for (size_t q = 0; q < k; ++q)
-        if (steps[q].kind == GS_DOUBLE && (L >> steps[q].i) / 4 <= c->dtail_max_quads) ++smalls;
-      if (got == H && smalls >= 2 && k == steps.size() - H / 2) {
-        steps.resize(k);
-        hostH = H;
+      for (uint32_t H = c->host_rounds & ~1u; H >= 2 && hostH == 0; H -= 2) {
+        size_t k = steps.size();
+        uint32_t got = 0;
+        while (got < H && k > 0 && steps[k - 1].kind == GS_DOUBLE && steps[k - 1].np == 2) {
+          --k;
+          got += 2;
+        }
+        size_t smalls = 0;  // device double steps left for the persistent tail
+        for (size_t q = 0; q < k; ++q)
+          if (steps[q].kind == GS_DOUBLE && (L >> steps[q].i) / 4 <= c->dtail_max_quads) ++smalls;
+        if (got == H && smalls >= 2 && k == steps.size() - H / 2) {
+          steps.resize(k);
+          hostH = H;
+        }
       }
     }
     // the small doubles (>= 2 of them) in one persistent kernel
@@ -1250,7 +1262,11 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         Fe e0, e2;
         host_round_sums<F>(T, e0, e2);
         one_round(i, e0, zk::hfe_sub<F>(claim, e0), e2);
-        if (i + 1 < nv) host_fold<F>(T, r);
+        if (i + 1 < nv || fin) host_fold<F>(T, r);
+      }
+      if (fin) {
+        for (int t = 0; t < 4; ++t) fin->v[t] = T[t][0];
+        fin->ok = true;
       }
       if (c->tail_trace)
         fprintf(stderr, "zk host rounds %u..%u: %.2f us (table copy %.2f us)\n", st.i, nv - 1,

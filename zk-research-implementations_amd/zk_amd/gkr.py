@@ -55,9 +55,15 @@ class Circuit:  # gkr_circuit.rs:107-144
         return out
 
     def _abi(self):
-        gates = np.array([len(layer) for layer in self.layers], np.uint32)
-        ops = np.array([int(op) for layer in self.layers for op in layer], np.uint8)
-        return gates, ops
+        # the C arrays of the structure, built once: like the reference's
+        # Circuit::new (gkr_circuit.rs:114-125) a circuit's layers are fixed
+        # after construction (replace `layers` to change it)
+        key = id(self.layers)
+        if getattr(self, "_abi_key", None) != key:
+            gates = np.array([len(layer) for layer in self.layers], np.uint32)
+            ops = np.fromiter((op for layer in self.layers for op in layer), np.uint8, int(gates.sum()))
+            self._abi_cache, self._abi_key = (gates, ops), key
+        return self._abi_cache
 
 
 @dataclass
@@ -84,8 +90,23 @@ def _rounds(gates: np.ndarray) -> int:
     return n.value
 
 
-def prove(circuit: Circuit, inputs: list[int], ctx: Context | None = None,
+def _layer_rounds(gates, coeffs, nco, ch, field):
+    """Per layer (output first): its round polynomials (trimmed) and challenges,
+    from the C arrays in one conversion each."""
+    flat, chs, cnt = to_ints(coeffs.reshape(-1, 4)), to_ints(ch), nco.tolist()
+    polys, chal, k0 = [], [], 0
+    for layer in reversed(range(len(gates))):
+        nv = 2 * (2 * int(gates[layer])).bit_length() - 2
+        polys.append([UnivariatePoly(flat[3 * k: 3 * k + cnt[k]], field) for k in range(k0, k0 + nv)])
+        chal.append(chs[k0: k0 + nv])
+        k0 += nv
+    return polys, chal
+
+
+def prove(circuit: Circuit, inputs: list[int] | np.ndarray, ctx: Context | None = None,
           taus: list[int] | None = None) -> GkrCircuitProof:  # :31-126
+    """gkr::prove. inputs: canonical ints, or a uint64[n, 4] array of them
+    (little-endian limbs, the C ABI layout) which skips their conversion."""
     ctx = ctx or default_context()
     if taus is not None:
         return _prove_kzg(circuit, inputs, ctx, taus)
@@ -98,15 +119,10 @@ def prove(circuit: Circuit, inputs: list[int], ctx: Context | None = None,
     ch = np.zeros((total, 4), np.uint64)
     claims = np.zeros((max(2 * (L - 1), 1), 4), np.uint64)
     ins = np.zeros((2, 4), np.uint64)
-    x = as_limbs([int(v) for v in inputs])
+    x = as_limbs(inputs)
     _call(lib().zk_gkr_circuit_prove(ctx.h, int(circuit.field), REPR_CANONICAL, L, ptr(gates), ptr(ops), ptr(x),
                                      len(inputs), ptr(outp), ptr(coeffs), ptr(nco), ptr(ch), ptr(claims), ptr(ins)))
-    polys, chal, k0 = [], [], 0
-    for layer in reversed(range(L)):
-        nv = 2 * (2 * int(gates[layer])).bit_length() - 2
-        polys.append([UnivariatePoly(to_ints(coeffs[k, : nco[k]]), circuit.field) for k in range(k0, k0 + nv)])
-        chal.append(to_ints(ch[k0: k0 + nv]))
-        k0 += nv
+    polys, chal = _layer_rounds(gates, coeffs, nco, ch, circuit.field)
     cl = to_ints(claims[: 2 * (L - 1)])
     return GkrCircuitProof(to_ints(outp), polys, [(cl[2 * i], cl[2 * i + 1]) for i in range(L - 1)],
                            tuple(to_ints(ins)), chal)
@@ -136,12 +152,7 @@ def _prove_kzg(circuit: Circuit, inputs: list[int], ctx: Context, taus: list[int
     _call(lib().zk_gkr_circuit_prove_kzg(ctx.h, REPR_CANONICAL, L, ptr(gates), ptr(ops), ptr(x), len(inputs),
                                          ptr(as_limbs([int(t) for t in taus])), ptr(outp), ptr(coeffs), ptr(nco),
                                          ptr(ch), ptr(claims), ptr(ins), ptr(com), ptr(prf), ptr(g2)))
-    polys, chal, k0 = [], [], 0
-    for layer in reversed(range(L)):
-        nv = 2 * (2 * int(gates[layer])).bit_length() - 2
-        polys.append([UnivariatePoly(to_ints(coeffs[k, : nco[k]]), circuit.field) for k in range(k0, k0 + nv)])
-        chal.append(to_ints(ch[k0: k0 + nv]))
-        k0 += nv
+    polys, chal = _layer_rounds(gates, coeffs, nco, ch, circuit.field)
     cl = to_ints(claims[: 2 * (L - 1)])
     opened = tuple(to_ints(ins))
     pts = _points(prf[: 2 * nin])
