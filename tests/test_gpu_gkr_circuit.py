@@ -97,6 +97,39 @@ def test_two_phase_equals_dense_tables(monkeypatch, field):
     assert proofs["0"] == proofs["1"] == proofs["host0"] == proofs["host10"]
 
 
+def test_bench_circuit_equals_dense_tables(monkeypatch):
+    """bench.py gkr_circuit's workload (4 096 inputs, seed 11, BN254 Fr): the
+    default prover (layers of <= 2^9 entries on the host, device layers of 2^10
+    .. 2^12 with host-round ends: 4, 2 and 4 of them, and evaluations from the
+    folds) equals the dense route (ZK_CIRCUIT_DENSE=1: L^2 tables, evaluations
+    by k_mle_eval2) and verifies; limb-array inputs give the same proof."""
+    import zk_amd
+    from zk_amd.elems import as_limbs
+
+    rng = random.Random(11)
+    log_inputs = 12
+    structure = [[rng.choice((Operation.Add, Operation.Mul)) for _ in range(1 << (log_inputs - 1 - i))]
+                 for i in range(log_inputs)]
+    inputs = [rng.randrange(go.MODULI[0]) for _ in range(1 << log_inputs)]
+    circ = Circuit(structure, 0)
+    got = {}
+    for dense in ("0", "1"):
+        monkeypatch.setenv("ZK_CIRCUIT_DENSE", dense)
+        monkeypatch.delenv("ZK_CIRCUIT_HOST_LGL", raising=False)
+        c = zk_amd.Context(0)
+        try:
+            pr = prove(circ, inputs, c)
+            got[dense] = ([[q.coefficient for q in layer] for layer in pr.proof_polynomials], pr.claimed_evaluations,
+                          pr.input_evaluations, pr.random_challenges)
+            if dense == "0":
+                assert verify(pr, circ, inputs)
+                pa = prove(circ, as_limbs(inputs), c)
+                assert pa.random_challenges == pr.random_challenges and pa.input_evaluations == pr.input_evaluations
+        finally:
+            c.close()
+    assert got["0"] == got["1"]
+
+
 @pytest.mark.parametrize("field", [0, 2])
 def test_large_circuit_verifies(ctx, field):
     rng = random.Random(77 + field)

@@ -33,6 +33,6 @@ for nv in map(int, sys.argv[1:]):
         ts.append(time.perf_counter() - t0)
     t_commit = sorted(ts)[1]
     print(f"nv {nv}: setup {t_setup * 1e3:.1f} ms, commit (2^{nv}-point MSM) {t_commit * 1e3:.2f} ms, "
-          f"{(1 << nv) / t_commit / 1e6:.1f} M points/s", flush=True)
+          f"{(1 << nv) / t_commit / 1e6:.1f} M points/s, commitment x lo {int(out[0][0]):016x}", flush=True)
     k.close()
     del dev

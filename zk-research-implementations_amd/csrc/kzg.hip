@@ -104,18 +104,28 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   const uint32_t cb = std::min<uint32_t>(20, std::max<uint32_t>(5, lg > 8 ? lg - 3 : 5));
   const uint32_t W = (255 + cb - 1) / cb;
   const uint64_t nb = (uint64_t)W << cb;
+  require((uint64_t)n * W < (1ull << 32), "MSM too large");  // u32 entry offsets
   DevBuf& cnt = c->msm[10];
   DevBuf& cur = c->msm[11];
   DevBuf& ord = c->msm[12];
   cnt.ensure((nb + 1) * 4);
-  cur.ensure(nb * 4);
   ord.ensure(std::max<uint64_t>(1, n * W) * 4);
-  HIPCK(hipMemsetAsync(cnt.p, 0, (nb + 1) * 4, c->stream));
-  const uint32_t g = grid_for(c, n, k_msm_count);
-  launch(c, ZK_K_MSM, 32.0 * n, 0, k_msm_count, g, scalars, n, cb, W, dptr<uint32_t>(cnt));
-  scan_u32(c, dptr<uint32_t>(cnt), nb + 1);
-  HIPCK(hipMemcpyAsync(cur.p, cnt.p, nb * 4, hipMemcpyDeviceToDevice, c->stream));
-  launch(c, ZK_K_MSM, 32.0 * n, 0, k_msm_scatter, g, scalars, n, cb, W, dptr<uint32_t>(cur), dptr<uint32_t>(ord));
+  {  // bucket sort (msm.hpp k_sort_hist / k_sort_scatter / k_sort_fine)
+    const uint32_t C = cb - sort_fine_bits(cb), nbin = W << C;
+    require(nbin <= kSortBinsMax, "internal: MSM coarse bins exceed the LDS table");
+    const uint32_t NB = (uint32_t)((n + kSortPts - 1) / kSortPts);
+    const uint64_t nh = (uint64_t)nbin * NB + 1;
+    cur.ensure(nh * 4);
+    DevBuf& ent = c->msm[16];
+    ent.ensure(std::max<uint64_t>(1, n * W) * 8);
+    HIPCK(hipMemsetAsync(cur.p, 0, nh * 4, c->stream));
+    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist, NB, scalars, n, cb, W, NB, dptr<uint32_t>(cur));
+    scan_u32(c, dptr<uint32_t>(cur), nh);
+    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, NB, (const uint32_t*)dptr<uint32_t>(cur),
+           dptr<uint64_t>(ent));
+    launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), cb, NB,
+           (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
+  }
   // bucket sums (mixed additions of the gathered affine bases)
   G1J* buckets = seg_reduce(c, bases, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
   // per window: sum_d d B_d over chunks of buckets, then over the chunks

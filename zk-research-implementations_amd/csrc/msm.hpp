@@ -5,9 +5,8 @@
 // MSM (Pippenger). The reference commits with a naive sum of n full scalar
 // multiplications (evaluate_poly_with_l_basis_in_g1, kzg.rs:131-144). Here:
 // scalars are cut into W = ceil(255 / c) windows of c bits; every nonzero
-// digit puts its point into bucket (w, d) (counting sort: histogram, scan,
-// scatter); buckets are summed by a segmented reduction (tasks of <= kSegTask
-// points, repeated over the partial sums until every bucket is one task, so a
+// digit puts its point into bucket (w, d) (a blocked counting sort, below);
+// buckets are summed by a segmented reduction (tasks of <= kSegTask points, repeated over the partial sums until every bucket is one task, so a
 // skewed scalar distribution — all equal, all zero — never serialises on one
 // thread); each window's sum_d d * B_d comes from running sums over chunks of
 // buckets; the host combines the W window sums (Horner, c doublings each).
@@ -66,29 +65,99 @@ __device__ __forceinline__ uint32_t scalar_digit(const Fe& s, uint32_t bit, uint
   if (wi + 1 < 8) x |= (uint64_t)s.v[wi + 1] << 32;
   return (uint32_t)(x >> sh) & ((1u << c) - 1u);
 }
-// counts[w * 2^c + d] += 1 for every point with digit d != 0 in window w
-__global__ __launch_bounds__(kBlock) void k_msm_count(const Fe* __restrict__ scalars, uint64_t n, uint32_t c, uint32_t W,
-                                                      uint32_t* __restrict__ counts) {
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+// The entries sorted by (window, digit) without a global atomic per entry (a
+// count / scan / scatter with one global atomic per entry took 8.2 + 21.6 ms
+// at 2^24 points against 0.5 + 3.2 + 5.6 ms here, round 4). Digits split
+// into C coarse and F fine bits (F = c / 2):
+//  1. k_sort_hist: block b counts its kSortPts points' entries per (window,
+//     coarse bin) in LDS and stores the counts bin-major, H[bin NB + b];
+//  2. an exclusive scan of H gives every block its run in every coarse bin;
+//  3. k_sort_scatter: the block writes (point << F | fine) into its runs (LDS
+//     cursors, runs of ~kSortPts / 2^C entries);
+//  4. k_sort_fine: one block per coarse bin counting-sorts its entries by the
+//     fine bits in LDS and writes the bucket offsets (the exclusive scan of the
+//     per-bucket counts, `cnt`) and the point order `ord`.
+// Within a bucket the order is arbitrary (LDS atomics): bucket sums are group
+// sums.
+constexpr uint32_t kSortPts = 16384;        // points per block in passes 1 and 3
+constexpr uint32_t kSortBinsMax = 14336;    // W 2^C over c = 5..20 (c = 19: 14 x 1024)
+__host__ __device__ __forceinline__ uint32_t sort_fine_bits(uint32_t c) { return c / 2; }
+__global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
+                                                      uint32_t W, uint32_t NB, uint32_t* __restrict__ H) {
+  __shared__ uint32_t hist[kSortBinsMax];
+  const uint32_t F = sort_fine_bits(c), C = c - F, nbin = W << C;
+  for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) hist[j] = 0;
+  __syncthreads();
+  const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
+  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
     const Fe s = ld_fe(scalars, i);
     for (uint32_t w = 0; w < W; ++w) {
       const uint32_t d = scalar_digit(s, w * c, c);
-      if (d) atomicAdd(counts + ((uint64_t)w << c) + d, 1u);
+      if (d) atomicAdd(&hist[(w << C) + (d >> F)], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) H[(uint64_t)j * NB + blockIdx.x] = hist[j];
+}
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
+                                                         uint32_t W, uint32_t NB, const uint32_t* __restrict__ Hs,
+                                                         uint64_t* __restrict__ E) {
+  __shared__ uint32_t cur[kSortBinsMax];
+  const uint32_t F = sort_fine_bits(c), C = c - F, nbin = W << C;
+  for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) cur[j] = Hs[(uint64_t)j * NB + blockIdx.x];
+  __syncthreads();
+  const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
+  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
+    const Fe s = ld_fe(scalars, i);
+    for (uint32_t w = 0; w < W; ++w) {
+      const uint32_t d = scalar_digit(s, w * c, c);
+      if (d) E[atomicAdd(&cur[(w << C) + (d >> F)], 1u)] = (i << F) | (d & ((1u << F) - 1u));
     }
   }
 }
-// order[cursor[key]++] = i (cursor = exclusive scan of counts)
-__global__ __launch_bounds__(kBlock) void k_msm_scatter(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
-                                                        uint32_t W, uint32_t* __restrict__ cursor,
-                                                        uint32_t* __restrict__ order) {
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    const Fe s = ld_fe(scalars, i);
-    for (uint32_t w = 0; w < W; ++w) {
-      const uint32_t d = scalar_digit(s, w * c, c);
-      if (d) order[atomicAdd(cursor + ((uint64_t)w << c) + d, 1u)] = (uint32_t)i;
+// grid = W 2^C blocks, one per coarse bin; cnt gets (W << c) + 1 offsets
+__global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict__ E, uint32_t c, uint32_t NB,
+                                                      const uint32_t* __restrict__ Hs, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ ord) {
+  __shared__ uint32_t h[1024];
+  __shared__ uint32_t part[kBlock];
+  const uint32_t F = sort_fine_bits(c), nf = 1u << F, bin = blockIdx.x, t = threadIdx.x;
+  const uint32_t start = Hs[(uint64_t)bin * NB], end = Hs[(uint64_t)(bin + 1) * NB];  // (H has one total entry past the bins)
+  for (uint32_t f = t; f < nf; f += kBlock) h[f] = 0;
+  __syncthreads();
+  for (uint32_t e = start + t; e < end; e += kBlock) atomicAdd(&h[(uint32_t)E[e] & (nf - 1u)], 1u);
+  __syncthreads();
+  // exclusive scan of h[0, nf): each thread scans its 4 (nf <= 1024), then the thread totals
+  uint32_t v[4], tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t f = 4 * t + k;
+    v[k] = f < nf ? h[f] : 0u;
+    tot += v[k];
+  }
+  part[t] = tot;
+  __syncthreads();
+  for (uint32_t off = 1; off < kBlock; off <<= 1) {
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = start + part[t] - tot;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t f = 4 * t + k;
+    if (f < nf) {
+      h[f] = run;  // becomes the cursor of fine digit f
+      cnt[((uint64_t)bin << F) + f] = run;
     }
+    run += v[k];
+  }
+  if (bin + 1 == gridDim.x && t == 0) cnt[(uint64_t)gridDim.x << F] = end;  // the total
+  __syncthreads();
+  for (uint32_t e = start + t; e < end; e += kBlock) {
+    const uint64_t x = E[e];
+    ord[atomicAdd(&h[(uint32_t)x & (nf - 1u)], 1u)] = (uint32_t)(x >> F);
   }
 }
 
