@@ -101,9 +101,14 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   require(n < (1ull << 28), "MSM too large");
   uint32_t lg = 0;
   while ((2ull << lg) <= n) ++lg;
-  const uint32_t cb = std::min<uint32_t>(20, std::max<uint32_t>(5, lg > 8 ? lg - 3 : 5));
-  const uint32_t W = (255 + cb - 1) / cb;
-  const uint64_t nb = (uint64_t)W << cb;
+  // c-bit signed digits (msm.hpp signed_digits): W c >= 256, 2^(c-1) buckets per window
+  // (c = log2 n - 3 in [6, 20], then evened out over its W windows so the top
+  // window is not a sliver: 17 -> 16 x 16 bits, 20 stays 13 x 20)
+  const uint32_t c0 = std::min<uint32_t>(20, std::max<uint32_t>(6, lg > 9 ? lg - 3 : 6));
+  const uint32_t W = (256 + c0 - 1) / c0;
+  const uint32_t cb = (256 + W - 1) / W;
+  const uint32_t bb = cb - 1;  // bucket key bits
+  const uint64_t nb = (uint64_t)W << bb;
   require((uint64_t)n * W < (1ull << 32), "MSM too large");  // u32 entry offsets
   DevBuf& cnt = c->msm[10];
   DevBuf& cur = c->msm[11];
@@ -111,7 +116,7 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   cnt.ensure((nb + 1) * 4);
   ord.ensure(std::max<uint64_t>(1, n * W) * 4);
   {  // bucket sort (msm.hpp k_sort_hist / k_sort_scatter / k_sort_fine)
-    const uint32_t C = cb - sort_fine_bits(cb), nbin = W << C;
+    const uint32_t C = bb - sort_fine_bits(bb), nbin = W << C;
     require(nbin <= kSortBinsMax, "internal: MSM coarse bins exceed the LDS table");
     const uint32_t NB = (uint32_t)((n + kSortPts - 1) / kSortPts);
     const uint64_t nh = (uint64_t)nbin * NB + 1;
@@ -123,19 +128,19 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
     scan_u32(c, dptr<uint32_t>(cur), nh);
     launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, NB, (const uint32_t*)dptr<uint32_t>(cur),
            dptr<uint64_t>(ent));
-    launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), cb, NB,
+    launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), bb, NB,
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
   }
   // bucket sums (mixed additions of the gathered affine bases)
   G1J* buckets = seg_reduce(c, bases, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
   // per window: sum_d d B_d over chunks of buckets, then over the chunks
-  const uint32_t chunks = (1u << cb) / kBucketChunk;
+  const uint32_t chunks = (1u << bb) / kBucketChunk;
   DevBuf& chb = c->msm[13];
-  chb.ensure((size_t)W * chunks * sizeof(G1J));
-  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * chunks), (const G1J*)buckets, cb, W,
+  chb.ensure((size_t)W * (chunks + 1) * sizeof(G1J));
+  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * (chunks + 1)), (const G1J*)buckets, bb, W,
          dptr<G1J>(chb));
   std::vector<uint32_t> woff(W + 1);
-  for (uint32_t w = 0; w <= W; ++w) woff[w] = w * chunks;
+  for (uint32_t w = 0; w <= W; ++w) woff[w] = w * (chunks + 1);
   DevBuf& wo = c->msm[14];
   wo.ensure((W + 1) * 4);
   HIPCK(hipMemcpyAsync(wo.p, woff.data(), (W + 1) * 4, hipMemcpyHostToDevice, c->stream));

@@ -19,7 +19,7 @@
 namespace zk {
 
 constexpr uint32_t kSegTask = 32;    // points summed by one thread per reduction level
-constexpr uint32_t kBucketChunk = 32;  // buckets per thread in the window reduction
+constexpr uint32_t kBucketChunk = 16;  // buckets per thread in the window reduction
 
 __device__ __forceinline__ Fq ld_fq(const Fq* p, uint64_t i) { return p[i]; }
 
@@ -59,43 +59,71 @@ __global__ __launch_bounds__(kBlock) void k_scan_add(uint32_t* __restrict__ a, u
 
 // ---- bucket sort --------------------------------------------------------------
 // digit w of a canonical 255-bit scalar (8 x u32 LE)
+// (words picked by selects: a dynamic index into s.v would put s in scratch)
+__device__ __forceinline__ uint32_t fe_word(const Fe& s, uint32_t k) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) r = k == j ? s.v[j] : r;
+  return r;
+}
 __device__ __forceinline__ uint32_t scalar_digit(const Fe& s, uint32_t bit, uint32_t c) {
   const uint32_t wi = bit >> 5, sh = bit & 31;
-  uint64_t x = s.v[wi];
-  if (wi + 1 < 8) x |= (uint64_t)s.v[wi + 1] << 32;
+  const uint64_t x = (uint64_t)fe_word(s, wi) | (uint64_t)fe_word(s, wi + 1) << 32;  // (word 8 reads as 0)
   return (uint32_t)(x >> sh) & ((1u << c) - 1u);
 }
-// The entries sorted by (window, digit) without a global atomic per entry (a
+// Signed digits (round 4): W windows of c bits with W c >= 256, each digit in
+// (-2^(c-1), 2^(c-1)] (a window above 2^(c-1) becomes negative and carries one
+// into the next; the last carry fits in the top window). A point goes to the
+// bucket of its digit's magnitude m — m mod 2^(c-1), so m = 2^(c-1) shares
+// bucket 0, which the host weighs separately — with y negated for a negative
+// digit: half the buckets of unsigned digits for the same additions.
+template <class Fn>
+__device__ __forceinline__ void signed_digits(const Fe& s, uint32_t c, uint32_t W, Fn&& f) {
+  const uint32_t half = 1u << (c - 1);
+  uint32_t carry = 0;
+  for (uint32_t w = 0; w < W; ++w) {
+    const uint32_t raw = scalar_digit(s, w * c, c) + carry;
+    const uint32_t neg = raw > half ? 1u : 0u;
+    carry = neg;
+    const uint32_t m = neg ? (1u << c) - raw : raw;
+    if (m) f(w, m & (half - 1u), neg);
+  }
+}
+// The entries sorted by (window, bucket) without a global atomic per entry (a
 // count / scan / scatter with one global atomic per entry took 8.2 + 21.6 ms
-// at 2^24 points against 0.5 + 3.2 + 5.6 ms here, round 4). Digits split
-// into C coarse and F fine bits (F = c / 2):
+// at 2^24 points against 0.5 + 3.2 + 5.6 ms here, round 4). Bucket keys
+// (b = c - 1 bits) split into C coarse = LOW bits and F fine = HIGH bits
+// (F = b / 2): the top window's keys are small (its digits hold the scalar's
+// last bits), and low coarse bits spread them over every bin. Buckets are
+// therefore stored at bucket_slot(key) = low << F | high (window sums read
+// them through it):
 //  1. k_sort_hist: block b counts its kSortPts points' entries per (window,
 //     coarse bin) in LDS and stores the counts bin-major, H[bin NB + b];
 //  2. an exclusive scan of H gives every block its run in every coarse bin;
-//  3. k_sort_scatter: the block writes (point << F | fine) into its runs (LDS
+//  3. k_sort_scatter: the block writes (point, sign, fine) into its runs (LDS
 //     cursors, runs of ~kSortPts / 2^C entries);
 //  4. k_sort_fine: one block per coarse bin counting-sorts its entries by the
 //     fine bits in LDS and writes the bucket offsets (the exclusive scan of the
-//     per-bucket counts, `cnt`) and the point order `ord`.
+//     per-bucket counts, `cnt`) and the point order `ord` (bit 31: negate).
 // Within a bucket the order is arbitrary (LDS atomics): bucket sums are group
 // sums.
 constexpr uint32_t kSortPts = 16384;        // points per block in passes 1 and 3
-constexpr uint32_t kSortBinsMax = 14336;    // W 2^C over c = 5..20 (c = 19: 14 x 1024)
-__host__ __device__ __forceinline__ uint32_t sort_fine_bits(uint32_t c) { return c / 2; }
+constexpr uint32_t kSortBinsMax = 13312;    // W 2^C over c = 6..20 (c = 20: 13 x 1024)
+__host__ __device__ __forceinline__ uint32_t sort_fine_bits(uint32_t b) { return b / 2; }
+__host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t b) {
+  const uint32_t F = sort_fine_bits(b), C = b - F;
+  return ((key & ((1u << C) - 1u)) << F) | (key >> C);
+}
 __global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
                                                       uint32_t W, uint32_t NB, uint32_t* __restrict__ H) {
   __shared__ uint32_t hist[kSortBinsMax];
-  const uint32_t F = sort_fine_bits(c), C = c - F, nbin = W << C;
+  const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = W << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) hist[j] = 0;
   __syncthreads();
   const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
-  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
-    const Fe s = ld_fe(scalars, i);
-    for (uint32_t w = 0; w < W; ++w) {
-      const uint32_t d = scalar_digit(s, w * c, c);
-      if (d) atomicAdd(&hist[(w << C) + (d >> F)], 1u);
-    }
-  }
+  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
+    signed_digits(ld_fe(scalars, i), c, W,
+                  [&](uint32_t w, uint32_t key, uint32_t) { atomicAdd(&hist[(w << C) + (key & ((1u << C) - 1u))], 1u); });
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) H[(uint64_t)j * NB + blockIdx.x] = hist[j];
 }
@@ -103,25 +131,22 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const Fe* __restrict__ 
                                                          uint32_t W, uint32_t NB, const uint32_t* __restrict__ Hs,
                                                          uint64_t* __restrict__ E) {
   __shared__ uint32_t cur[kSortBinsMax];
-  const uint32_t F = sort_fine_bits(c), C = c - F, nbin = W << C;
+  const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = W << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) cur[j] = Hs[(uint64_t)j * NB + blockIdx.x];
   __syncthreads();
   const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
-  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
-    const Fe s = ld_fe(scalars, i);
-    for (uint32_t w = 0; w < W; ++w) {
-      const uint32_t d = scalar_digit(s, w * c, c);
-      if (d) E[atomicAdd(&cur[(w << C) + (d >> F)], 1u)] = (i << F) | (d & ((1u << F) - 1u));
-    }
-  }
+  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
+    signed_digits(ld_fe(scalars, i), c, W, [&](uint32_t w, uint32_t key, uint32_t neg) {
+      E[atomicAdd(&cur[(w << C) + (key & ((1u << C) - 1u))], 1u)] = (i << (F + 1)) | ((uint64_t)neg << F) | (key >> C);
+    });
 }
-// grid = W 2^C blocks, one per coarse bin; cnt gets (W << c) + 1 offsets
-__global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict__ E, uint32_t c, uint32_t NB,
+// grid = W 2^C blocks, one per coarse bin; cnt gets (W << b) + 1 offsets (b: bucket bits)
+__global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict__ E, uint32_t b, uint32_t NB,
                                                       const uint32_t* __restrict__ Hs, uint32_t* __restrict__ cnt,
                                                       uint32_t* __restrict__ ord) {
   __shared__ uint32_t h[1024];
   __shared__ uint32_t part[kBlock];
-  const uint32_t F = sort_fine_bits(c), nf = 1u << F, bin = blockIdx.x, t = threadIdx.x;
+  const uint32_t F = sort_fine_bits(b), nf = 1u << F, bin = blockIdx.x, t = threadIdx.x;
   const uint32_t start = Hs[(uint64_t)bin * NB], end = Hs[(uint64_t)(bin + 1) * NB];  // (H has one total entry past the bins)
   for (uint32_t f = t; f < nf; f += kBlock) h[f] = 0;
   __syncthreads();
@@ -157,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict
   __syncthreads();
   for (uint32_t e = start + t; e < end; e += kBlock) {
     const uint64_t x = E[e];
-    ord[atomicAdd(&h[(uint32_t)x & (nf - 1u)], 1u)] = (uint32_t)(x >> F);
+    ord[atomicAdd(&h[(uint32_t)x & (nf - 1u)], 1u)] = (uint32_t)(x >> (F + 1)) | ((uint32_t)(x >> F) & 1u) << 31;
   }
 }
 
@@ -194,7 +219,12 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
   const uint32_t b = a + kSegTask < e ? a + kSegTask : e;
   G1J acc = g1_inf();
   for (uint32_t j = a; j < b; ++j) {
-    if (GATHER) acc = g1_add_mixed(acc, bases[order[j]]);
+    if (GATHER) {  // order bit 31: the point's digit is negative
+      const uint32_t o = order[j];
+      G1A p = bases[o & 0x7fffffffu];
+      if (o >> 31) p.y = fq_neg(p.y);
+      acc = g1_add_mixed(acc, p);
+    }
     else acc = g1_add(acc, items[j]);
   }
   out[t] = acc;
@@ -202,20 +232,29 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
 
 // ---- window reduction -----------------------------------------------------------
 // For window w, chunk j of buckets d in [lo, hi): sum_d d B_d = u + lo * T with
-// T = sum B_d, u = sum (d - lo) B_d (running sum from the top).
+// T = sum B_d, u = sum (d - lo) B_d (running sum from the top), at
+// out[w (chunks + 1) + j]; W more threads put 2^c B_0 (bucket 0 holds the
+// digits of magnitude 2^c, signed_digits) at out[w (chunks + 1) + chunks].
 __global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict__ buckets, uint32_t c, uint32_t W,
                                                           G1J* __restrict__ out) {
   const uint32_t chunks = (1u << c) / kBucketChunk;
   const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-  if (g >= W * chunks) return;
-  const uint32_t w = g / chunks, lo = (g % chunks) * kBucketChunk, hi = lo + kBucketChunk;
+  if (g >= W * (chunks + 1)) return;
+  if (g >= W * chunks) {
+    const uint32_t w = g - W * chunks;
+    G1J z = buckets[(uint64_t)w << c];
+    for (uint32_t k = 0; k < c; ++k) z = g1_dbl(z);
+    out[w * (chunks + 1) + chunks] = z;
+    return;
+  }
+  const uint32_t w = g / chunks, j = g % chunks, lo = j * kBucketChunk, hi = lo + kBucketChunk;
   const G1J* B = buckets + ((uint64_t)w << c);
   G1J t = g1_inf(), u = g1_inf();
   for (uint32_t d = hi; d-- > lo;) {
-    t = g1_add(t, B[d]);
+    t = g1_add(t, B[bucket_slot(d, c)]);
     if (d > lo) u = g1_add(u, t);
   }
-  out[g] = lo ? g1_add(u, g1_mul_small(t, lo)) : u;  // d = 0 (lo = 0) has weight 0: u already is sum d B_d
+  out[w * (chunks + 1) + j] = lo ? g1_add(u, g1_mul_small(t, lo)) : u;  // d = 0 (lo = 0) has weight 0 here
 }
 
 // ---- fixed-base scalar multiplication (Lagrange basis setup) ----------------------
