@@ -169,9 +169,9 @@ def test_verify_random_12_var_opening(ctx):
 def test_full_size_commit_equals_mle_value_times_g(ctx, n):
     """BASELINE config 5 at full size (kzg.rs:51-53,131-144): the commitment of
     the bench's 2^n-point table through zk_dev_kzg_commit, whose window width
-    grows with n (kzg.hip msm_g1_device: c = 19 at 2^22 with 14 windows, 20
-    at 2^24 with 13 windows of 2^20 buckets — parameters the small tests never
-    reach), equals
+    grows with n (kzg.hip msm_g1_device: signed digits, c = 19 at 2^22 with
+    14 windows, 20 at 2^24 with 13 windows of 2^19 buckets, the top window's
+    digits small — parameters the small tests never reach), equals
     f(taus) * G1 from the C oracle's MLE evaluation, and the committed fixture
     (tests/golden/kzg.json, tests/golden/make_kzg_golden.py)."""
     import json
