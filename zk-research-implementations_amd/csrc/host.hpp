@@ -169,6 +169,14 @@ struct DevBuf {
   }
   Fe* fe(size_t off_elems = 0) const { return reinterpret_cast<Fe*>(p) + off_elems; }
 };
+// a temporary device buffer, freed when it goes out of scope (error paths too)
+struct ScopedBuf {
+  DevBuf b;
+  ScopedBuf() = default;
+  ScopedBuf(const ScopedBuf&) = delete;
+  ScopedBuf& operator=(const ScopedBuf&) = delete;
+  ~ScopedBuf() { b.release(); }
+};
 
 enum CommKind { COMM_NONE = 0, COMM_HOST = 1, COMM_RCCL = 2 };
 }  // namespace zkh

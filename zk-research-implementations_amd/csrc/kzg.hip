@@ -210,14 +210,13 @@ const G1A* g1_fixed_table16(zk_ctx* c) {
   if (c->g1_table16.p) return dptr<G1A>(c->g1_table16);
   const G1A* t8 = g1_fixed_table(c);
   const uint64_t n = 16ull * kFB16;
-  DevBuf jac;
-  jac.ensure(n * sizeof(G1J));
-  launch(c, ZK_K_MSM, 0, 0, k_table16, grid_for(c, n, k_table16), t8, dptr<G1J>(jac));
+  ScopedBuf jac;
+  jac.b.ensure(n * sizeof(G1J));
+  launch(c, ZK_K_MSM, 0, 0, k_table16, grid_for(c, n, k_table16), t8, dptr<G1J>(jac.b));
   c->g1_table16.ensure(n * sizeof(G1A));
   launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
-         (const G1J*)dptr<G1J>(jac), n, dptr<G1A>(c->g1_table16));
+         (const G1J*)dptr<G1J>(jac.b), n, dptr<G1A>(c->g1_table16));
   sync(c);
-  jac.release();
   return dptr<G1A>(c->g1_table16);
 }
 
@@ -229,14 +228,13 @@ const G1A* g1_fixed_table20(zk_ctx* c) {
   if (c->g1_table20.p) return dptr<G1A>(c->g1_table20);
   const G1A* t16 = g1_fixed_table16(c);
   const uint64_t n = (uint64_t)kFB20W * kFB20;
-  DevBuf jac;
-  jac.ensure(n * sizeof(G1J));
-  launch(c, ZK_K_MSM, 0, 0, k_table20, grid_for(c, n, k_table20), t16, dptr<G1J>(jac));
+  ScopedBuf jac;
+  jac.b.ensure(n * sizeof(G1J));
+  launch(c, ZK_K_MSM, 0, 0, k_table20, grid_for(c, n, k_table20), t16, dptr<G1J>(jac.b));
   c->g1_table20.ensure(n * sizeof(G1A));
   launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
-         (const G1J*)dptr<G1J>(jac), n, dptr<G1A>(c->g1_table20));
+         (const G1J*)dptr<G1J>(jac.b), n, dptr<G1A>(c->g1_table20));
   sync(c);
-  jac.release();
   c->g1_table16.release();
   return dptr<G1A>(c->g1_table20);
 }

@@ -273,8 +273,10 @@ __global__ __launch_bounds__(kBlock) void k_table16(const G1A* __restrict__ t8, 
 // 20-bit signed windows (round 4): table20[w * 2^19 + j] = m * 2^(20w) * G with
 // m = j (j >= 1) or 2^19 (j = 0), the magnitudes of signed_digits(c = 20, W =
 // 13); built from table16 with one mixed addition per entry (a 20-bit range at
-// bit 20w spans at most two 16-bit windows: 20w mod 16 is 0, 4, 8 or 12).
-// out[i] = scalars[i] * G with 13 mixed additions instead of 16.
+// bit 20w spans at most two 16-bit windows: 20w mod 16 is 0, 4, 8 or 12; the
+// top window's entries are exact for m < 2^16 — a scalar below 2^255, as every
+// canonical Fr is, gives it magnitudes <= 2^15).
+// out[i] = scalars[i] * G (canonical scalars) with 13 mixed additions instead of 16.
 constexpr uint32_t kFB20 = 1u << 19, kFB20W = 13;
 __global__ __launch_bounds__(kBlock) void k_table20(const G1A* __restrict__ t16, G1J* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
