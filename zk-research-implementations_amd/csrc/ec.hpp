@@ -208,6 +208,45 @@ ZK_HD G1J g1_add(const G1J& p, const G1J& q) {  // add-2007-bl
   return r;
 }
 
+// XYZZ accumulators (round 4): (X, Y, ZZ, ZZZ) is the affine point (X/ZZ,
+// Y/ZZZ) with ZZ^3 = ZZZ^2; ZZ = 0 is infinity. Adding an affine point costs
+// 8 multiplications + 2 squarings (madd-2008-s) against 7 + 4 for Jacobian
+// madd-2007-bl, and a run of additions converts to Jacobian once (3 + 4).
+struct G1XYZZ {
+  Fq X, Y, ZZ, ZZZ;
+};
+ZK_HD G1XYZZ g1x_inf() { return {fq_zero(), fq_zero(), fq_zero(), fq_zero()}; }
+ZK_HD G1XYZZ g1x_dbl(const G1XYZZ& p) {  // dbl-2008-s-1 (a = 0)
+  if (fq_is_zero(p.ZZ)) return p;
+  const Fq U = fq_dbl(p.Y), V = fq_sqr(U), W = fq_mul(U, V), S = fq_mul(p.X, V);
+  const Fq X2 = fq_sqr(p.X), M = fq_add(fq_dbl(X2), X2);
+  G1XYZZ r;
+  r.X = fq_sub(fq_sqr(M), fq_dbl(S));
+  r.Y = fq_sub(fq_mul(M, fq_sub(S, r.X)), fq_mul(W, p.Y));
+  r.ZZ = fq_mul(V, p.ZZ);
+  r.ZZZ = fq_mul(W, p.ZZZ);
+  return r;
+}
+ZK_HD G1XYZZ g1x_add_mixed(const G1XYZZ& p, const G1A& q) {  // madd-2008-s
+  if (g1a_is_inf(q)) return p;
+  if (fq_is_zero(p.ZZ)) return {q.x, q.y, fq_one(), fq_one()};
+  const Fq P = fq_sub(fq_mul(q.x, p.ZZ), p.X), R = fq_sub(fq_mul(q.y, p.ZZZ), p.Y);
+  if (fq_is_zero(P)) return fq_is_zero(R) ? g1x_dbl(p) : g1x_inf();
+  const Fq PP = fq_sqr(P), PPP = fq_mul(P, PP), Q = fq_mul(p.X, PP);
+  G1XYZZ r;
+  r.X = fq_sub(fq_sub(fq_sqr(R), PPP), fq_dbl(Q));
+  r.Y = fq_sub(fq_mul(R, fq_sub(Q, r.X)), fq_mul(p.Y, PPP));
+  r.ZZ = fq_mul(p.ZZ, PP);
+  r.ZZZ = fq_mul(p.ZZZ, PPP);
+  return r;
+}
+// Jacobian with Z' = ZZ ZZZ (= Z^5 for Z^2 = ZZ): X' = X ZZ^4, Y' = Y ZZZ^4
+ZK_HD G1J g1x_to_jac(const G1XYZZ& p) {
+  if (fq_is_zero(p.ZZ)) return g1_inf();
+  const Fq a = fq_sqr(p.ZZ), b = fq_sqr(p.ZZZ);
+  return {fq_mul(p.X, fq_sqr(a)), fq_mul(p.Y, fq_sqr(b)), fq_mul(p.ZZ, p.ZZZ)};
+}
+
 ZK_HD G1A g1_to_affine(const G1J& p) {
   if (g1_is_inf(p)) return {fq_zero(), fq_zero()};
   const Fq zi = fq_inv(p.Z), zi2 = fq_sqr(zi);

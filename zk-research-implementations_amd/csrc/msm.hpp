@@ -217,17 +217,20 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
   const uint32_t s = task_seg[t], k = t - task_off[s];
   const uint32_t a = off[s] + k * kSegTask, e = off[s + 1];
   const uint32_t b = a + kSegTask < e ? a + kSegTask : e;
-  G1J acc = g1_inf();
-  for (uint32_t j = a; j < b; ++j) {
-    if (GATHER) {  // order bit 31: the point's digit is negative
+  if constexpr (GATHER) {  // XYZZ accumulator over affine points (ec.hpp); order bit 31: negative digit
+    G1XYZZ acc = g1x_inf();
+    for (uint32_t j = a; j < b; ++j) {
       const uint32_t o = order[j];
       G1A p = bases[o & 0x7fffffffu];
       if (o >> 31) p.y = fq_neg(p.y);
-      acc = g1_add_mixed(acc, p);
+      acc = g1x_add_mixed(acc, p);
     }
-    else acc = g1_add(acc, items[j]);
+    out[t] = g1x_to_jac(acc);
+  } else {
+    G1J acc = g1_inf();
+    for (uint32_t j = a; j < b; ++j) acc = g1_add(acc, items[j]);
+    out[t] = acc;
   }
-  out[t] = acc;
 }
 
 // ---- window reduction -----------------------------------------------------------
@@ -292,13 +295,13 @@ __global__ __launch_bounds__(kBlock) void k_fixed_base20(const G1A* __restrict__
                                                          uint64_t n, G1J* __restrict__ out) {
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    G1J acc = g1_inf();
+    G1XYZZ acc = g1x_inf();
     signed_digits(ld_fe(scalars, i), 20, kFB20W, [&](uint32_t w, uint32_t key, uint32_t neg) {
       G1A p = table[(uint64_t)w * kFB20 + key];
       if (neg) p.y = fq_neg(p.y);
-      acc = g1_add_mixed(acc, p);
+      acc = g1x_add_mixed(acc, p);
     });
-    out[i] = acc;
+    out[i] = g1x_to_jac(acc);
   }
 }
 
