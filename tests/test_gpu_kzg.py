@@ -122,6 +122,31 @@ def test_msm_arbitrary_bases(ctx):
     assert msm_g1([], [], ctx) is None
 
 
+def test_msm_ragged_multi_block_signed_digits(ctx):
+    """An MSM whose length is not a power of two and spans three blocks of the
+    bucket sort (msm.hpp kSortPts = 16 384, the last one partial), over a few
+    repeated bases (equal points meet in a bucket: the XYZZ doubling and
+    cancellation cases), with scalars that hit the signed-digit edges: every
+    window at 2^(c-1) (bucket 0's magnitude), every bit set (a carry through
+    every window), r - 1, 0 and 1. Oracle: sum_i s_i k_i * G for bases k_i G."""
+    rng = random.Random(21)
+    n = 2 * 16384 + 777  # c = 12: 22 windows, 2^11 buckets each
+    ks = [1, 2, 3, 5, 8, 13, 21]
+    pts = [ko.mul(k, ko.G1) for k in ks]
+    c = 12
+    half_all = sum(1 << (c * w + c - 1) for w in range((256 + c - 1) // c)) % R
+    special = [half_all, (1 << 255) - 1, R - 1, 0, 1, (1 << 11), (1 << 12) - 1]
+    scalars = [rng.randrange(R) for _ in range(n)]
+    for i, v in enumerate(special * 50):
+        scalars[(i * 977) % n] = v % R
+    bases = [pts[i % len(ks)] for i in range(n)]
+    want = sum(s * ks[i % len(ks)] for i, s in enumerate(scalars)) % R
+    assert msm_g1(bases, scalars, ctx) == ko.mul(want, ko.G1)
+    # all one point (every entry of a window in one bucket) and a cancelling pair
+    assert msm_g1([pts[0]] * 20000, [3] * 20000, ctx) == ko.mul(60000, ko.G1)
+    assert msm_g1([pts[1], pts[1]], [5, R - 5], ctx) is None
+
+
 def test_invalid_inputs(ctx):
     with pytest.raises(ValueError, match="not on the curve"):
         msm_g1([(1, 2)], [1], ctx)
