@@ -557,7 +557,10 @@ def main() -> None:
     lg = (world - 1).bit_length()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+        import datetime
+
+        # (a rank that fails leaves the others at a barrier: fail within minutes, not torch's 30)
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
         if args.comm == "host":
             from zk_amd.dist import TorchAllreduce
 
