@@ -39,7 +39,8 @@ class Operation(IntEnum):  # multilinear_polynomial_evaluation.rs:4-17
 
 class Circuit:  # gkr_circuit.rs:107-144
     def __init__(self, structure: list[list[Operation]], field: int = Field.BN254_FR):
-        self.layers = [[Operation(op) for op in layer] for layer in structure]
+        # immutable, like the reference's Circuit after Circuit::new (gkr_circuit.rs:114-125)
+        self.layers = tuple(tuple(Operation(op) for op in layer) for layer in structure)
         self.field = Field(field)
 
     def evaluate(self, inputs: list[int]) -> list[list[int]]:  # :127-143 (host; O(#gates))
@@ -55,14 +56,12 @@ class Circuit:  # gkr_circuit.rs:107-144
         return out
 
     def _abi(self):
-        # the C arrays of the structure, built once: like the reference's
-        # Circuit::new (gkr_circuit.rs:114-125) a circuit's layers are fixed
-        # after construction (replace `layers` to change it)
-        key = id(self.layers)
-        if getattr(self, "_abi_key", None) != key:
+        # the C arrays of the structure, built once (the layers are tuples;
+        # assigning a new `layers` rebuilds them)
+        if getattr(self, "_abi_src", None) is not self.layers:  # (holds the source: no id reuse)
             gates = np.array([len(layer) for layer in self.layers], np.uint32)
             ops = np.fromiter((op for layer in self.layers for op in layer), np.uint8, int(gates.sum()))
-            self._abi_cache, self._abi_key = (gates, ops), key
+            self._abi_cache, self._abi_src = (gates, ops), self.layers
         return self._abi_cache
 
 
