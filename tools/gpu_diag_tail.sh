@@ -1,6 +1,6 @@
 # Per-step loop times (ZK_DEBUG_TAIL) of the 24-var proof for the default library and
 # diagnostic variants in abtest/ (wrong proofs allowed: seed 7 has no fixture).
-# usage: ENV="ZK_D0Q=1" bash tools/gpu_diag_tail.sh abtest/a.so abtest/b.so ...
+# usage: ENV="ZK_HOST_ROUNDS=6" bash tools/gpu_diag_tail.sh abtest/a.so abtest/b.so ...
 set -o pipefail
 mkdir -p gpurun_out
 for lib in "" "$@"; do

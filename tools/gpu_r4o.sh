@@ -1,4 +1,5 @@
-# Round 4: blocked MSM bucket sort (ZK_MSM_SORT=1, default) against the atomic scatter (0):
+# Round 4 (record; the ZK_MSM_SORT knob and the atomic scatter were removed after this A/B):
+# blocked MSM bucket sort (ZK_MSM_SORT=1) against the atomic scatter (0):
 # KZG parity (incl. 2^22 / 2^24 against the golden commitments), then commit timings and a rocprof.
 set -o pipefail
 mkdir -p gpurun_out

@@ -83,7 +83,7 @@ __device__ __forceinline__ void st_row(uint8_t* row, const Fe& x) {
 
 // ---------------------------------------------------------------------------
 // k_gkr_d0m: rounds 0 and 1 from the input tables in one pass (the step of
-// k_gkr_d0r, same nine categories and limb-sum output) with the products on
+// the removed VALU k_gkr_d0r: nine categories, limb-sum output) with the products on
 // the matrix cores. Wave w of a block serves product pp = w & 1 (0: A*S,
 // 1: M*P) over its own sequence of chunks of 32 quads (waves 0-1 and 2-3
 // take alternate chunks), so every input byte is loaded once. Per chunk lane
@@ -96,7 +96,7 @@ __device__ __forceinline__ void st_row(uint8_t* row, const Fe& x) {
 // category in LDS (int64), then per category the signed integer
 //   G = sum_d T_d 2^(8d) + M,  M = p 2^275 > |G| (a multiple of p: G stays
 // congruent), normalised to 17 non-negative 32-bit words — the unreduced
-// 17-word product sum of the VALU kernels — and grid_finish as k_gkr_d0r.
+// 17-word product sum of the VALU kernels — and grid_finish.
 // Bounds: |C| <= 2^19 per chunk, so a wave takes at most kD0MChunksMax
 // chunks (int32 tiles); |G| < 2 * 2^16 * 2^510 < M < 2^530 for a block.
 // ---------------------------------------------------------------------------
