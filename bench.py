@@ -69,11 +69,16 @@ def proof_check(field: int, n: int, seed: int, coeffs, nco, ch) -> dict:
     full-size oracle fixture for this workload (tests/golden/large.json, from
     oracle/zk_oracle.c or_gkr_prove_fast via tests/golden/make_large_golden.py)
     when one exists. A mismatch aborts the bench: a wrong proof has no rate."""
-    import zk_amd
     from zk_amd.elems import to_ints
 
-    polys = [to_ints(coeffs[k, : nco[k]]) for k in range(n)]
-    chal = to_ints(ch)
+    return proof_digest_check(field, n, seed, [to_ints(coeffs[k, : nco[k]]) for k in range(n)], to_ints(ch))
+
+
+def proof_digest_check(field: int, n: int, seed: int, polys, chal, abort: bool = True) -> dict:
+    """proof_check on a proof given as Python ints (trimmed coefficient lists
+    per round, challenges)."""
+    import zk_amd
+
     p = zk_amd.modulus(field)
     c = polys[0] + [0] * (3 - len(polys[0]))
     claimed = (2 * c[0] + c[1] + c[2]) % p
@@ -84,7 +89,7 @@ def proof_check(field: int, n: int, seed: int, coeffs, nco, ch) -> dict:
     fix = json.load(open(path)).get(key) if os.path.exists(path) else None
     out = {"blob_keccak256": dig, "fixture": f"tests/golden/large.json[{key}]" if fix else None,
            "matches_oracle_fixture": (dig == fix["blob_keccak256"]) if fix else None}
-    if fix and dig != fix["blob_keccak256"]:
+    if abort and fix and dig != fix["blob_keccak256"]:
         raise SystemExit(f"proof digest {dig} != oracle fixture {fix['blob_keccak256']} ({key})")
     return out
 
@@ -224,8 +229,14 @@ def cpu_baseline(field: int, nvars: int, fast_nvars: int) -> dict:
 
     tabs = [co.synth(field, 3, t, 0, 1 << nvars) for t in range(4)]
     t0 = time.perf_counter()
-    co.gkr_prove(field, tabs, co.Transcript())
+    polys, chal = co.gkr_prove(field, tabs, co.Transcript())
     dt = time.perf_counter() - t0
+    # the reference-faithful port's proof pins the committed full-size fixture
+    # (written by the fused restatement): abort unless the two agree
+    port_check = proof_digest_check(field, nvars, 3, polys, chal, abort=False)
+    if port_check["matches_oracle_fixture"] is False:
+        raise SystemExit(f"reference-faithful CPU port's proof digest {port_check['blob_keccak256']} != "
+                         f"{port_check['fixture']}")
     ops = 32.0 * ((1 << nvars) - 1)
     del tabs
     # the fast restatement (fused, in place, OpenMP on every thread this
@@ -251,6 +262,8 @@ def cpu_baseline(field: int, nvars: int, fast_nvars: int) -> dict:
         "sample": f"one gkr_prove over a {nvars}-var synthetic SumPoly (4 tables x 2^{nvars}), "
         f"{dt:.2f} s single-thread, host '{cpu_model()}' ({os.cpu_count()} logical CPUs)",
         "prover_ms_sample": dt * 1e3,
+        "matches_fixture": port_check["matches_oracle_fixture"],
+        "port_proof": port_check,
         "fast_allcores": {
             "value": 32.0 * ((1 << nf) - 1) / dtf,
             "unit": "field-ops/s",
@@ -517,8 +530,92 @@ def config4_bench(ctx, field: int, world: int, rank: int, barrier, total_nvars: 
     }
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, cmd: list, env_extra: dict | None = None, grace_s: float = 10.0,
+                poll_s: float = 0.2) -> tuple[int, str]:
+    """Launcher for `bench.py --gpus N` run without torch.distributed.run: start
+    `cmd` as N fresh child processes, one per GPU, with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torchrun would set), and
+    wait for all of them. The caller (the parent) never imports torch or touches
+    the GPU: it is a launcher, not a re-exec. Rank 0's stdout is captured
+    (the bench's one JSON line); every other stream goes to the parent's stderr.
+    When a rank exits non-zero the others are given `grace_s` to finish, then
+    killed (their peers would otherwise wait at a barrier). Returns (exit code,
+    rank 0's stdout): 0 only if every rank exited 0, else the first failing
+    rank's code (a signal death maps to 128 + signal)."""
+    import signal
+
+    env0 = dict(os.environ)
+    env0.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(_free_port()), "ZK_BENCH_LAUNCHER": "self"})
+    env0.update(env_extra or {})
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen(cmd, env=env, stdin=subprocess.DEVNULL,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True))
+    import threading
+
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    first_bad, t_bad = None, None
+    while True:
+        codes = [p.poll() for p in procs]
+        if first_bad is None:
+            for r, c in enumerate(codes):
+                if c is not None and c != 0:
+                    first_bad, t_bad = r, time.monotonic()
+                    print(f"bench launcher: rank {r} exited with {c}", file=sys.stderr)
+                    break
+        if all(c is not None for c in codes):
+            break
+        if first_bad is not None and time.monotonic() - t_bad > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)  # the rank's own session (start_new_session)
+                    except ProcessLookupError:
+                        pass
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(poll_s)
+    reader.join(timeout=30)
+    text = out0[0].decode(errors="replace") if out0 and out0[0] else ""
+    codes = [p.returncode for p in procs]
+    if first_bad is None:
+        bad = [c for c in codes if c != 0]
+        rc = bad[0] if bad else 0
+    else:
+        rc = codes[first_bad]
+    if rc < 0:
+        rc = 128 - rc
+    return rc, text
+
+
 def main() -> None:
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch: N fresh rank processes of this script (the parent never
+        # imports torch or touches a GPU); rank 0's JSON line is relayed
+        rc, text = spawn_ranks(args.gpus, [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:])
+        lines = [ln for ln in text.splitlines() if ln.strip()]
+        if rc == 0 and lines:
+            sys.stdout.write(lines[-1] + "\n")
+            sys.stdout.flush()
+        elif rc == 0:
+            print("bench launcher: rank 0 printed no result line", file=sys.stderr)
+            rc = 1
+        raise SystemExit(rc)
     # stdout carries exactly ONE line, the JSON result: libraries that print
     # banners to stdout (RCCL's "RCCL version ..." at communicator init) are
     # sent to stderr by pointing fd 1 there; the result goes to the saved fd.
@@ -529,8 +626,8 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks (torch.distributed.run "
+                         "--nproc-per-node N, or plain `python bench.py --gpus N`, which starts them itself)")
     field = FIELDS[args.field]
 
     import ctypes as C
@@ -687,6 +784,9 @@ def main() -> None:
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
             traffic_src = f"profiles/r4_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.4f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
+    comm = ctx.comm_info()  # what the attached communicator reports (RCCL: ncclCommCount / ncclCommUserRank)
+    if comm["kind"] != "none" and (comm["count"] != world or comm["rank"] != rank):
+        raise SystemExit(f"communicator reports rank {comm['rank']} of {comm['count']}, expected {rank} of {world}")
     if rank == 0:
         out = {
             "metric": "GKR sum-check field-ops/sec + prover ms, 24-var BN254, 1/2/4/8 GPU",
@@ -712,6 +812,9 @@ def main() -> None:
                    "host (gloo) all-reduce per round: diagnostic, not the product path") if world > 1 else "single GPU",
             },
             "proof": digest,
+            "comm": comm,
+            "rccl_ranks": comm["count"] if comm["kind"] == "rccl" else None,
+            "launcher": os.environ.get("ZK_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
             "roofline": {
                 "bound": "hbm",
                 "kernel": round_kinds.get(dom, dom) + "; the longest launch of the proof",

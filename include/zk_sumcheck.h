@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 12u
+#define ZK_ABI_VERSION 13u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -380,6 +380,11 @@ int zk_ctx_attach_host_comm(zk_ctx* ctx, int rank, int world, zk_allreduce_u64_f
 int zk_comm_get_unique_id(uint8_t out[128]);
 int zk_ctx_attach_rccl(zk_ctx* ctx, int rank, int world, const uint8_t unique_id[128]);
 int zk_ctx_detach_comm(zk_ctx* ctx);
+/* The communicator the ctx holds: *out_kind = 0 none, 1 host callback, 2 RCCL;
+ * *out_rank / *out_count = this rank and the number of ranks — for RCCL as the
+ * communicator reports them (ncclCommUserRank / ncclCommCount), else the
+ * attached rank / world (0 / 1 with none). */
+int zk_ctx_comm_count(const zk_ctx* ctx, int* out_kind, int* out_rank, int* out_count);
 /* gkr_prove over the global (nvars_local + log2(world))-variable SumPoly whose
  * local shard this rank holds; outputs are the global proof (identical on all
  * ranks). out arrays sized for nvars_local + log2(world) rounds. */

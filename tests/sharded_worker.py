@@ -2,6 +2,7 @@
 tests/test_gpu_sharded.py; not a test module itself).
 
 env: RANK, WORLD_SIZE, MASTER_PORT, COMM in {host, rccl, none}, FIELD, NLOCAL, OUT
+(+ optional SEED, default 19)
 Rank g proves its low-index-bit shard; rank 0 writes the proof as JSON.
 """
 from __future__ import annotations
@@ -34,7 +35,8 @@ def main() -> None:
     elif comm == "rccl":
         rendezvous_rccl(ctx, rank, world)
     i0, stride = shard_layout(rank, world)
-    tabs = [ctx.synth(field, 1 << nloc, seed=19, table=t, index0=i0, stride=stride) for t in range(4)]
+    seed = int(os.environ.get("SEED", "19"))
+    tabs = [ctx.synth(field, 1 << nloc, seed=seed, table=t, index0=i0, stride=stride) for t in range(4)]
     n = nloc + world.bit_length() - 1
     arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
     coeffs = np.zeros((max(n, 1), 3, 4), np.uint64)
@@ -44,10 +46,16 @@ def main() -> None:
     check(lib().zk_dev_gkr_sumcheck_prove_sharded(ctx.h, field, arr, nloc, 0, ptr(as_limbs([0])), tr.h, ptr(coeffs),
                                                   ptr(nco), ptr(ch)))
     polys = [to_ints(coeffs[k, : nco[k]]) for k in range(n)]
+    for t in tabs:
+        t.free()
     blob = zk_amd.GkrProof([zk_amd.UnivariatePoly(p, field) for p in polys], 0, []).to_bytes(field)
+    c = (polys[0] + [0, 0, 0])[:3] if n else [0, 0, 0]
+    claimed = (2 * c[0] + c[1] + c[2]) % zk_amd.modulus(field)  # s_0(0) + s_0(1), as the fixtures hold it
+    blob_c = zk_amd.GkrProof([zk_amd.UnivariatePoly(p, field) for p in polys], claimed, []).to_bytes(field)
     res = {"polys": [[hex(x) for x in p] for p in polys],
            "chal": [hex(x) for x in to_ints(ch[:n])], "collectives": ctx.stats()["collectives"],
-           "blob_keccak": zk_amd.keccak256(blob).hex()}
+           "blob_keccak": zk_amd.keccak256(blob).hex(), "blob_keccak_claimed": zk_amd.keccak256(blob_c).hex(),
+           "comm": ctx.comm_info()}
     with open(os.path.join(os.environ["OUT"], f"rank{rank}.json"), "w") as fh:
         json.dump(res, fh)
     dist.barrier()

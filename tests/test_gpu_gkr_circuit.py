@@ -185,3 +185,17 @@ def test_reference_circuit_with_input_kzg(ctx, taus):
     assert not verify(dataclasses.replace(got, input_proof=bad_prf), circ)
     with pytest.raises(ValueError):
         prove(Circuit([[OPS[o] for o in layer] for layer in structure], 0), inputs, ctx, taus=taus)
+
+
+def test_input_kzg_accepts_limb_array_inputs(ctx):
+    """prove() documents inputs as Python ints or the C ABI's uint64[n, 4]
+    limb array; with taus (the KZG path) the array must give the same proof
+    as the ints (the KZG path used to int() each row)."""
+    from zk_amd.elems import as_limbs
+
+    structure = [[A, A, A, A], [M, A], [A]]
+    inputs = [5, 2, 2, 4, 10, 0, 3, 3]
+    circ = Circuit([[OPS[o] for o in layer] for layer in structure], 2)
+    a = prove(circ, inputs, ctx, taus=[5, 2, 3])
+    b = prove(circ, as_limbs(inputs), ctx, taus=[5, 2, 3])
+    assert a == b

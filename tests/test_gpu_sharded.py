@@ -18,6 +18,7 @@ import sys
 import pytest
 
 import coracle as co
+import gkr_schedule
 import pyoracle as po
 
 pytestmark = pytest.mark.gpu
@@ -59,49 +60,8 @@ def _oracle(field: int, n: int) -> dict:
             "blob_keccak": po.keccak256(po.proof_blob(po.BLOB_GKR, field, 0, [list(p) for p in polys])).hex()}
 
 
-def _bounds(nloc: int, d0: bool = True) -> list[int]:
-    """End round of each step of a sharded phase (no persistent steps across
-    ranks), as host.hpp gkr_phase builds the schedule."""
-    b: list[int] = []
-    if nloc == 0:
-        return b
-    if d0 and nloc >= 11:
-        nt, k = -1, 0
-        while 3 + 3 * k + 8 <= nloc:
-            r = nloc - 3 - 3 * k
-            if r % 2 == 0 and (r >= 12 or nt < 0):
-                nt = k
-            k += 1
-        b = [3 + 3 * k for k in range(nt + 1)] + [5 + 3 * nt]
-        i = 5 + 3 * nt
-    elif d0 and nloc >= 2 and nloc % 2 == 0:
-        b, i = [2], 2
-    else:
-        b, i = [1], 1
-        if nloc >= 2:
-            i += 1
-            b.append(i)
-        if nloc >= 3 and (nloc - 2) % 2 == 1:
-            i += 1
-            b.append(i)
-    while i + 1 < nloc:
-        i += 2
-        b.append(i)
-    return b
-
-
-def _collectives(nloc: int, gather_vars: int = 10, d0: bool = True) -> int:
-    """All-reduces of a sharded proof (world > 1): one per step until the
-    first step boundary leaving <= gather_vars local rounds, then ONE gather
-    of the folded tables (host.hpp gkr_prove_device); every later round runs
-    locally on every rank. Without such a boundary: every step + the final
-    gather of one element per table."""
-    b = _bounds(nloc, d0)
-    if gather_vars > 0:
-        for s, e in enumerate(b):
-            if e < nloc and nloc - e <= gather_vars:
-                return s + 1 + 1
-    return len(b) + 1
+# the schedule (steps, gather boundary, collective count) the library builds
+_bounds, _collectives = gkr_schedule.bounds, gkr_schedule.collectives
 
 
 # (2, 20, 0): each rank's first kernel fills the card (512 blocks) while the
@@ -181,3 +141,22 @@ def test_world8_host_comm_matches_single_process(tmp_path, nloc, field, gather):
     for rank, r in enumerate(res):
         assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
         assert r["collectives"] == _collectives(nloc, int(gather)), f"rank {rank}"
+
+
+def test_config4_workload_8_ranks_matches_fixture(tmp_path):
+    """BASELINE config 4's exact workload: the 26-variable seed-4 tables split
+    over 8 ranks (23 local variables each: 8 x 1 GiB of tables on this one
+    card, host all-reduce over gloo in place of RCCL). Every rank's proof must
+    equal the committed full-size fixture (tests/golden/large.json
+    bn254_fr_26_s4: round polynomials, challenges, blob digest), with the
+    shipped collective schedule (per-step all-reduces, then the early gather)."""
+    import json as _json
+
+    fix = _json.load(open(os.path.join(ROOT, "tests", "golden", "large.json")))["bn254_fr_26_s4"]
+    res = _run(8, "host", 0, 23, str(tmp_path), {"SEED": "4"})
+    for rank, r in enumerate(res):
+        assert r["polys"] == [[hex(int(c, 16)) for c in p] for p in fix["round_polys"]], f"rank {rank}"
+        assert r["chal"] == [hex(int(c, 16)) for c in fix["challenges"]], f"rank {rank}"
+        assert r["blob_keccak_claimed"] == fix["blob_keccak256"], f"rank {rank}"
+        assert r["collectives"] == _collectives(23), f"rank {rank}"
+        assert r["comm"] == {"kind": "host", "rank": rank, "count": 8}

@@ -197,3 +197,37 @@ def test_oracle_scale_and_binop():  # multilinear_polynomial_evaluation.rs:93-97
     assert po.binop(p, [1, 2, 3, 4], [5, 6], "add") == [6, 8]
     assert po.binop(p, [1, 2], [5, 6, 7, 8], "sub") == [p - 4, p - 4]
     assert po.binop(p, [2, 3], [4, 5], "mul") == [8, 15]
+
+
+@pytest.mark.slow
+def test_ref_port_pins_large_fixture():
+    """tests/golden/large.json was written by the fused restatement
+    (or_gkr_prove_fast). The reference-faithful port (or_gkr_prove: the
+    allocation-per-round algorithm of sum_check_protocol.rs:86-166) reproduces
+    the committed 23-variable fixture — round polynomials, challenges and the
+    proof blob digest (pyoracle's independent blob writer) — so the full-size
+    fixtures do not rest on the fast restatement alone (bench.py's cpu_baseline
+    does the same at 24 variables on the GPU box)."""
+    import json
+    import os
+
+    fix = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "large.json")))["bn254_fr_23_s3"]
+    n, seed, field = fix["nvars"], fix["seed"], fix["field"]
+    tabs = [co.synth(field, seed, t, 0, 1 << n) for t in range(4)]
+    polys, chal = co.gkr_prove(field, tabs, co.Transcript())
+    del tabs
+    assert polys == [[h2i(c) for c in p] for p in fix["round_polys"]]
+    assert chal == [h2i(c) for c in fix["challenges"]]
+    c = polys[0] + [0] * (3 - len(polys[0]))
+    claimed = (2 * c[0] + c[1] + c[2]) % po.MODULI[field]  # s(0) + s(1)
+    assert claimed == h2i(fix["claimed_sum"])
+    blob = po.proof_blob(po.BLOB_GKR, field, claimed, polys)
+    assert po.keccak256(blob).hex() == fix["blob_keccak256"]
+
+
+@pytest.mark.slow
+def test_ref_port_equals_fast_restatement_21():
+    """The two restatements agree above the golden sizes (21 variables, every
+    step kind of the fast schedule)."""
+    tabs = [co.synth(0, 9, t, 0, 1 << 21) for t in range(4)]
+    assert co.gkr_prove(0, tabs, co.Transcript()) == co.gkr_prove(0, tabs, co.Transcript(), fast=True)

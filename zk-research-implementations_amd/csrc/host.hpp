@@ -1298,6 +1298,12 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
           memcpy(rd.v, lg.r[j], 32);
           const uint32_t m = lg.m[j];
           if (m > 3) fail(ZK_EDEVICE, "device Fiat-Shamir record corrupt");
+          for (uint32_t q = m; q < 3; ++q) cf[q] = zk::fe_zero<F>();
+          // the device's interpolation, checked: s(0) + s(1) = 2 c0 + c1 + c2 must be
+          // the running claim (a replayed hash alone proves only the replay)
+          const Fe s01 = zk::hfe_add<F>(zk::hfe_add<F>(zk::hfe_add<F>(cf[0], cf[0]), cf[1]), cf[2]);
+          if (memcmp(s01.v, claim.v, 32) != 0)
+            fail(ZK_EDEVICE, "device Fiat-Shamir round polynomial does not match the running claim");
           const uint32_t k = k0 + st.i + 2 * d + j;
           absorb<F>(tr, cf, m);
           out.ncoeffs[k] = (uint8_t)m;

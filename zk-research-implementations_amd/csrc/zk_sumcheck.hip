@@ -643,6 +643,20 @@ int zk_ctx_detach_comm(zk_ctx* c) {
     c->comm = COMM_NONE;
   });
 }
+int zk_ctx_comm_count(const zk_ctx* c, int* out_kind, int* out_rank, int* out_count) {
+  return guarded([&] {
+    require(c && out_kind && out_rank && out_count, "null argument");
+    int n = c->world, r = c->rank;
+    if (c->comm == COMM_RCCL) {  // what the communicator itself reports
+      require(c->nccl != nullptr, "RCCL communicator missing");
+      NCCLCK(ncclCommCount(c->nccl, &n));
+      NCCLCK(ncclCommUserRank(c->nccl, &r));
+    }
+    *out_kind = static_cast<int>(c->comm);
+    *out_rank = r;
+    *out_count = n;
+  });
+}
 int zk_dev_gkr_sumcheck_prove_sharded(zk_ctx* c, zk_field field, const void* const d_local_tables[4],
                                       uint32_t nvars_local, zk_repr repr, const zk_fe* claimed_sum,
                                       zk_transcript* transcript, zk_fe* out_coeffs, uint8_t* out_ncoeffs,

@@ -113,6 +113,14 @@ class Context:
         check(lib().zk_ctx_detach_comm(self.h))
         self._callbacks = None
 
+    def comm_info(self) -> dict:
+        """{"kind": "none"|"host"|"rccl", "rank": r, "count": n}; for RCCL the
+        rank and count are what the communicator reports (ncclCommUserRank /
+        ncclCommCount)."""
+        kind, rank, count = C.c_int(), C.c_int(), C.c_int()
+        check(lib().zk_ctx_comm_count(self.h, C.byref(kind), C.byref(rank), C.byref(count)))
+        return {"kind": ("none", "host", "rccl")[kind.value], "rank": rank.value, "count": count.value}
+
 
 def rccl_unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()

@@ -147,7 +147,7 @@ def _prove_kzg(circuit: Circuit, inputs: list[int], ctx: Context, taus: list[int
     com = np.zeros((1, 12), np.uint64)
     prf = np.zeros((max(2 * nin, 1), 12), np.uint64)
     g2 = np.zeros((max(nin, 1), 24), np.uint64)
-    x = as_limbs([int(v) for v in inputs])
+    x = as_limbs(inputs)  # Python ints or the C ABI layout uint64[n, 4], as on the plain path
     _call(lib().zk_gkr_circuit_prove_kzg(ctx.h, REPR_CANONICAL, L, ptr(gates), ptr(ops), ptr(x), len(inputs),
                                          ptr(as_limbs([int(t) for t in taus])), ptr(outp), ptr(coeffs), ptr(nco),
                                          ptr(ch), ptr(claims), ptr(ins), ptr(com), ptr(prf), ptr(g2)))
