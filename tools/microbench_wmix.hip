@@ -9,6 +9,7 @@
 //   R16  : 16 inputs per output (fold by four), no stores
 //   W16  : 16 inputs -> 1 output (134 MB written)
 // and (round 4) R8 / W8 with the inputs landed in LDS by LDS-DMA (k_mix_glds).
+// Round 5: `mb_wmix calib` (see calib() below).
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/mb_wmix tools/microbench_wmix.hip
 #include <hip/hip_runtime.h>
 
@@ -16,6 +17,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                   \
@@ -33,6 +35,12 @@ struct Tabs {
   const uint4* in[4];
   uint4* out[4];
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+}
 
 __device__ __forceinline__ void xr(uint4& a, const uint4& c) {
   a.x ^= c.x;
@@ -119,7 +127,10 @@ float run(const Tabs& t, size_t O, int grid, int reps) {
 // i-th contiguous KiB of the wave's 2 KiB run: whole lines per instruction)
 // instead of the kernel's element-per-lane shape (lane l: bytes 32 l .. 32 l + 31
 // in two 16-B instructions, each touching every line of the run half)
-template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false>
+// RUN (round 5): each wave writes its chunk's NF folds as ONE contiguous run
+// (output index (ch NF + f) 64 + l: 16 KiB per chunk and table) instead of NF
+// runs of 2 KiB spread over the level-3 table; NTS: non-temporal stores
+template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false, bool RUN = false, bool NTS = false>
 __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const uint4* __restrict__ X = t.in[w];
@@ -158,8 +169,11 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
         xr(a, ca[k]);
         xr(b, cb[k]);
       }
-      const size_t e = ch * 64 + l + (size_t)f * O;
-      if (ST && STC) {
+      const size_t e = RUN ? (ch * NF + f) * 64 + l : ch * 64 + l + (size_t)f * O;
+      if (ST && NTS) {
+        nt_store(&X2[2 * e], a);
+        nt_store(&X2[2 * e + 1], b);
+      } else if (ST && STC) {
         const size_t r = ch * 64 + (size_t)f * O;
         X2[2 * r + l] = a;
         X2[2 * r + 64 + l] = b;
@@ -173,7 +187,7 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
   }
 }
 
-template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false>
+template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false, bool RUN = false, bool NTS = false>
 float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   const size_t in_max = (O - 1) + (size_t)(NF - 1) * O + (size_t)(NIN - 1) * NF * O, out_max = NF * O - 1;
   if (O % 64 || in_max >= (1ull << 24) || out_max >= (1ull << 24) / 8) {
@@ -186,7 +200,7 @@ float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   std::vector<float> v;
   for (int r = 0; r < reps; ++r) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_mix_pf<NIN, NF, ST, LDC, STC>), dim3(grid), dim3(256), 0, 0, t, O);
+    hipLaunchKernelGGL((k_mix_pf<NIN, NF, ST, LDC, STC, RUN, NTS>), dim3(grid), dim3(256), 0, 0, t, O);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -296,7 +310,94 @@ __global__ __launch_bounds__(256) void k_copy(Tabs t, size_t n4) {
   for (size_t i = (size_t)blockIdx.x * 64 + l; i < n4; i += (size_t)gridDim.x * 64) Y[i] = X[i];
 }
 
-int main() {
+// calibration copy (round 5): U uint4 per lane in flight (all U loads issued
+// before the U stores), lane-contiguous; NT: non-temporal stores
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_copyu(Tabs t, size_t n4) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* __restrict__ X = t.in[w];
+  uint4* __restrict__ Y = t.out[w];
+  const size_t step = (size_t)gridDim.x * 64 * U;
+  for (size_t i = (size_t)blockIdx.x * 64 * U + l; i < n4; i += step) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = X[i + 64 * k];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (NT)
+        nt_store(&Y[i + 64 * k], v[k]);
+      else
+        Y[i + 64 * k] = v[k];
+    }
+  }
+}
+template <int U, bool NT>
+float run_copyu(const Tabs& t, size_t n4, int grid, int reps) {
+  if (n4 % (64 * U)) exit(1);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> v;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_copyu<U, NT>), dim3(grid), dim3(256), 0, 0, t, n4);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    v.push_back(ms * 1000.f);
+  }
+  std::sort(v.begin(), v.end());
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return v[v.size() / 2];
+}
+
+// round 5: `mb_wmix calib` — copies of 4 x 512 MiB (2 GiB read + 2 GiB written)
+// at 1-4 blocks per CU, 1 or 4 uint4 per lane in flight, plain / non-temporal
+// stores; then the first t33 pattern (W8, one fold ahead as the kernel) with
+// today's output layout (eight 2 KiB runs per wave and chunk) against one
+// contiguous 16 KiB run per wave and chunk, plain and non-temporal.
+int calib() {
+  const size_t N = 1ull << 24;
+  Tabs t;
+  for (int i = 0; i < 4; ++i) {
+    uint4* p;
+    CK(hipMalloc(&p, N * 32));
+    CK(hipMemset(p, 0x11 * (i + 1), N * 32));
+    t.in[i] = p;
+    CK(hipMalloc(&t.out[i], N * 32));
+    CK(hipMemset(t.out[i], 0, N * 32));
+  }
+  const int reps = 7;
+  const size_t n4 = N * 2;  // uint4 per table: 512 MiB
+  const double bytes = 2.0 * 4 * n4 * 16;
+  for (int grid : {256, 512, 1024, 2048, 4096}) {
+    const float a = run_copyu<1, false>(t, n4, grid, reps), b = run_copyu<4, false>(t, n4, grid, reps);
+    const float c = run_copyu<1, true>(t, n4, grid, reps), d = run_copyu<4, true>(t, n4, grid, reps);
+    printf("copy 2 GiB + 2 GiB, grid %4d: U1 %7.1f us %.2f TB/s | U4 %7.1f %.2f | U1 nt %7.1f %.2f | U4 nt %7.1f %.2f\n", grid,
+           a, bytes / a / 1e6, b, bytes / b / 1e6, c, bytes / c / 1e6, d, bytes / d / 1e6);
+    fflush(stdout);
+  }
+  const size_t O8 = N / 64;
+  const double rd = 4.0 * N * 32, wr8 = 4.0 * N / 8 * 32;
+  for (int grid : {256, 512}) {
+    const float r8 = run_pf<8, 8, false>(t, O8, grid, reps);
+    const float w8 = run_pf<8, 8, true>(t, O8, grid, reps);
+    const float w8r = run_pf<8, 8, true, false, false, true>(t, O8, grid, reps);
+    const float w8n = run_pf<8, 8, true, false, false, false, true>(t, O8, grid, reps);
+    const float w8rn = run_pf<8, 8, true, false, false, true, true>(t, O8, grid, reps);
+    printf("t33 pattern (one fold ahead), grid %d: R8 %6.1f us (%.2f TB/s) | W8 2 KiB runs %6.1f (%.2f) | W8 16 KiB run "
+           "%6.1f (%.2f) | W8 nt %6.1f (%.2f) | W8 16 KiB run nt %6.1f (%.2f)\n",
+           grid, r8, rd / r8 / 1e6, w8, (rd + wr8) / w8 / 1e6, w8r, (rd + wr8) / w8r / 1e6, w8n, (rd + wr8) / w8n / 1e6,
+           w8rn, (rd + wr8) / w8rn / 1e6);
+    fflush(stdout);
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "calib") return calib();
   const size_t N = 1ull << 24;  // elements per input table
   Tabs t;
   for (int i = 0; i < 4; ++i) {
