@@ -222,3 +222,31 @@ def test_full_size_commit_equals_mle_value_times_g(ctx, n):
     assert got == ko.mul(v, ko.G1)
     fix = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kzg.json")))[f"bls12_381_fr_{n}_s5"]
     assert got == (int(fix["commit_x"], 16), int(fix["commit_y"], 16))
+
+
+def test_setup_tables_agree_across_threshold(ctx):
+    """Setups below 2^16 points build their basis from the 8-bit fixed-base
+    table (k_fixed_base8), larger ones from the 20-bit signed-window table that
+    every context on the device shares (kzg.hip FixedBaseCache): the
+    15-variable suffix basis of a 16-variable setup equals a 15-variable
+    setup's basis, and a second context's 16-variable setup (cached table)
+    commits to the same point."""
+    import zk_amd
+
+    rng = random.Random(16)
+    taus = [rng.randrange(R) for _ in range(16)]
+    k16 = KZG(taus, ctx)
+    k15 = KZG(taus[1:], ctx)
+    assert k16.lagrange_basis(15) == k15.lagrange_basis()
+    evals = [rng.randrange(R) for _ in range(1 << 16)]
+    c = k16.commit(evals)
+    assert c == ko.mul(po.evaluate(R, evals, taus), ko.G1)
+    ctx2 = zk_amd.Context(0)
+    try:
+        k2 = KZG(taus, ctx2)
+        assert k2.commit(evals) == c
+        k2.close()
+    finally:
+        ctx2.close()
+    k16.close()
+    k15.close()

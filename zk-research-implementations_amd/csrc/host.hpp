@@ -246,7 +246,7 @@ struct zk_ctx {
   DevBuf scan_tmp[4];
   DevBuf g1_table;
   DevBuf g1_table16;  // 16-bit windows (100 MB), built on the device from g1_table
-  DevBuf g1_table20;  // 20-bit signed windows (654 MB), built on the device from g1_table16
+  // (the 20-bit signed-window table, 654 MB, is cached per device for the process: kzg.hip FixedBaseCache)
 };
 
 

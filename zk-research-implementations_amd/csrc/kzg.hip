@@ -1,4 +1,7 @@
 // Multilinear KZG over BLS12-381 G1: host driver and C ABI.
+#include <map>
+#include <mutex>
+
 #include "host.hpp"
 #include "msm.hpp"
 #include "pairing.hpp"
@@ -221,23 +224,47 @@ const G1A* g1_fixed_table16(zk_ctx* c) {
 }
 
 // table20[w * 2^19 + j]: the 13 signed 20-bit windows' magnitudes (msm.hpp
-// k_table20), affine, built once per ctx from table16 (6.8 M mixed additions,
-// one batch normalisation); table16 is released afterwards
+// k_table20), affine, built from table16 (6.8 M mixed additions, one batch
+// normalisation; table16 is released afterwards) ONCE PER DEVICE AND PROCESS:
+// every context on the device shares it (654 MB, kept until the process
+// exits — it depends on nothing but the curve's generator). Round 4 rebuilt
+// it per context (cold setup 125 ms against 76 ms warm).
+struct FixedBaseCache {
+  std::mutex m;
+  std::map<int, void*> table20;  // device -> affine table (never freed: process lifetime)
+};
+FixedBaseCache& fixed_base_cache() {
+  static FixedBaseCache* cache = new FixedBaseCache();  // (leaked on purpose: no teardown order with the HIP runtime)
+  return *cache;
+}
 const G1A* g1_fixed_table20(zk_ctx* c) {
   using namespace zk;
-  if (c->g1_table20.p) return dptr<G1A>(c->g1_table20);
+  FixedBaseCache& fc = fixed_base_cache();
+  std::lock_guard<std::mutex> lock(fc.m);
+  auto it = fc.table20.find(c->device);
+  if (it != fc.table20.end()) return static_cast<const G1A*>(it->second);
   const G1A* t16 = g1_fixed_table16(c);
   const uint64_t n = (uint64_t)kFB20W * kFB20;
   ScopedBuf jac;
   jac.b.ensure(n * sizeof(G1J));
   launch(c, ZK_K_MSM, 0, 0, k_table20, grid_for(c, n, k_table20), t16, dptr<G1J>(jac.b));
-  c->g1_table20.ensure(n * sizeof(G1A));
-  launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
-         (const G1J*)dptr<G1J>(jac.b), n, dptr<G1A>(c->g1_table20));
-  sync(c);
+  DevBuf t20;  // owned by the cache once built
+  t20.ensure(n * sizeof(G1A));
+  try {
+    launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
+           (const G1J*)dptr<G1J>(jac.b), n, dptr<G1A>(t20));
+    sync(c);
+  } catch (...) {
+    t20.release();
+    throw;
+  }
   c->g1_table16.release();
-  return dptr<G1A>(c->g1_table20);
+  fc.table20[c->device] = t20.p;
+  return dptr<G1A>(t20);
 }
+// below this many basis points a setup uses the 8-bit table (k_fixed_base8:
+// 32 mixed additions per point) instead of building / holding table20
+constexpr uint64_t kSetupTable20Min = 1ull << 16;
 
 zk_g1 g1_out(const G1J& p) {
   const G1A a = zk::g1_to_affine(p);
@@ -368,7 +395,8 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
     k->nv = nvars;
     k->device = c->device;
     const uint64_t N = (uint64_t)1 << nvars, total = 2 * N - 1;  // every suffix level, level v at 2^v - 1
-    const G1A* table = g1_fixed_table20(c);
+    const bool big = N >= kSetupTable20Min;
+    const G1A* table = big ? g1_fixed_table20(c) : g1_fixed_table(c);
     DevBuf& tb = c->msm[14];
     tb.ensure(nvars * 32);
     upload<Fr381>(c, repr, taus, nvars, reinterpret_cast<Fe*>(tb.p));
@@ -383,8 +411,12 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
     } jac;
     jac.b.ensure(total * sizeof(G1J));
     G1J* J = dptr<G1J>(jac.b);
-    launch(c, ZK_K_MSM, 176.0 * N, 0, zk::k_fixed_base20, grid_for(c, N, zk::k_fixed_base20), table,
-           (const Fe*)sc.p, N, J + (N - 1));
+    if (big)
+      launch(c, ZK_K_MSM, 176.0 * N, 0, zk::k_fixed_base20, grid_for(c, N, zk::k_fixed_base20), table,
+             (const Fe*)sc.p, N, J + (N - 1));
+    else
+      launch(c, ZK_K_MSM, 128.0 * N, 0, zk::k_fixed_base8, grid_for(c, N, zk::k_fixed_base8), table,
+             (const Fe*)sc.p, N, J + (N - 1));
     // G2 half of run_trusted_setup (:43-46): tau_i * G2, on the host (nvars
     // scalar multiplications) while the basis kernels run
     {

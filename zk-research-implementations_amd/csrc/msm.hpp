@@ -305,6 +305,23 @@ __global__ __launch_bounds__(kBlock) void k_fixed_base20(const G1A* __restrict__
   }
 }
 
+// small setups (round 5): out[i] = scalars[i] * G from the 8-bit table
+// (t8[w * 256 + d] = d 2^(8w) G, 32 windows, 786 KB): 32 mixed additions per
+// point, no 654 MB table20 for a handful of basis points
+__global__ __launch_bounds__(kBlock) void k_fixed_base8(const G1A* __restrict__ t8, const Fe* __restrict__ scalars,
+                                                        uint64_t n, G1J* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const Fe s = ld_fe(scalars, i);
+    G1XYZZ acc = g1x_inf();
+    for (uint32_t w = 0; w < 32; ++w) {
+      const uint32_t d = (fe_word(s, w >> 2) >> (8 * (w & 3))) & 0xffu;
+      if (d) acc = g1x_add_mixed(acc, t8[w * 256 + d]);
+    }
+    out[i] = g1x_to_jac(acc);
+  }
+}
+
 // eq(taus, i) over n variables, MSB first (get_lagrange_basis's scalars, kzg.rs:183-206); canonical out
 template <class F>
 __global__ __launch_bounds__(kBlock) void k_eq_scalars(const Fe* __restrict__ taus, uint32_t nv, uint64_t count,

@@ -113,7 +113,6 @@ void zk_ctx_destroy(zk_ctx* c) {
   for (auto& b : c->scan_tmp) b.release();
   c->g1_table.release();
   c->g1_table16.release();
-  c->g1_table20.release();
   if (c->h_red) (void)hipHostFree(c->h_red);
   if (c->h_tab) (void)hipHostFree(c->h_tab);
   if (c->h_fslog) (void)hipHostFree(c->h_fslog);
