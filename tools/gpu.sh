@@ -19,6 +19,8 @@
 #   profile=TAG      rocprofv3 kernel trace + stats of the headline (tools/profile_bench.sh TAG)
 #   kzg              config 5 (BLS12-381 GKR + KZG commit) only
 #   mb=NAME[:ARGS]   run tools/mb_NAME (a prebuilt microbenchmark) with ARGS
+#   checks           the GPU parity files against the -DZK_DEVICE_CHECKS build
+#                    (make -C zk-research-implementations_amd checks; ZK_LIB_PATH)
 #   abenv=C1/C2/...  alternate bench configurations (each a comma-separated VAR=VAL list,
 #                    "-" = defaults), REPS (default 5) rounds of 30 timed proofs each;
 #                    prints ms per proof and the launch times of the event-timed proof
@@ -110,6 +112,15 @@ for step in "$@"; do
       [ "$margs" = "$arg" ] && margs=""
       timeout -k 10 300 ./tools/mb_$prog $margs > gpurun_out/mb_$prog.log 2>&1 || fail $step $? gpurun_out/mb_$prog.log
       cat gpurun_out/mb_$prog.log | tail -40 ;;
+    checks)
+      export ZK_LIB_PATH=$PWD/zk-research-implementations_amd/zk_amd/_lib_checks/libzksumcheck.so
+      [ -f "$ZK_LIB_PATH" ] || { echo "build the checks library first"; exit 1; }
+      timeout -k 10 1100 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_large.py tests/test_gpu_prelaunch.py \
+        tests/test_gpu_kzg.py tests/test_gpu_tables.py tests/test_gpu_gkr_circuit.py tests/test_gpu_device_fs.py \
+        -m gpu -x -q --timeout 300 --timeout-method thread > $log 2>&1 || fail $step $? $log
+      grep -c "zk device check failed" $log || true
+      tail -2 $log
+      unset ZK_LIB_PATH ;;
     abenv)
       IFS='/' read -ra cfgs <<< "$arg"
       for rep in $(seq 1 ${REPS:-5}); do

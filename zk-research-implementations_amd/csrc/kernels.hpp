@@ -15,6 +15,25 @@ namespace zk {
 
 constexpr int kBlock = 256;  // 4 waves of 64
 
+// Device bounds checks (debug build only: make -C
+// zk-research-implementations_amd checks, -DZK_DEVICE_CHECKS): every table
+// index of the matrix-core and MSM kernels is asserted against the table's
+// length; a failure prints the condition, block and thread, then traps.
+#ifdef ZK_DEVICE_CHECKS
+#define ZK_DCHECK(cond)                                                                                          \
+  do {                                                                                                           \
+    if (!(cond)) {                                                                                               \
+      printf("zk device check failed: %s (%s:%d) block %u thread %u\n", #cond, __FILE__, __LINE__, blockIdx.x, \
+             threadIdx.x);                                                                                       \
+      __builtin_trap();                                                                                          \
+    }                                                                                                            \
+  } while (0)
+#else
+#define ZK_DCHECK(cond) \
+  do {                  \
+  } while (0)
+#endif
+
 __device__ __forceinline__ Fe ld_fe(const Fe* __restrict__ p, uint64_t i) {
   const uint4* q = reinterpret_cast<const uint4*>(p) + 2 * i;
   const uint4 a = q[0], b = q[1];

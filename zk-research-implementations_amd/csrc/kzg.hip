@@ -59,8 +59,8 @@ uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + zk
 // Sum each segment s = items [off[s], off[s+1]) (device u32 offsets, nseg + 1).
 // Level 0 reads affine bases[order[j]] (order != null) or Jacobian items0[j].
 // Uses c->msm[pool .. pool+4]; returns a device pointer to nseg sums.
-G1J* seg_reduce(zk_ctx* c, const G1A* bases, const uint32_t* order, const G1J* items0, const uint32_t* off,
-                uint64_t nseg, int pool) {
+G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* order, const G1J* items0,
+                const uint32_t* off, uint64_t nseg, int pool) {
   const G1J* items = items0;
   bool gather = order != nullptr;
   const uint32_t* cur_off = off;
@@ -83,10 +83,10 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, const uint32_t* order, const G1J* i
            dptr<uint32_t>(tseg));
     part.ensure((size_t)total * sizeof(G1J));
     if (gather)
-      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<true>, blocks_for(total), bases, order, (const G1J*)nullptr, cur_off,
+      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<true>, blocks_for(total), bases, nbases, order, (const G1J*)nullptr, cur_off,
              (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg), total, dptr<G1J>(part));
     else
-      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<false>, blocks_for(total), (const G1A*)nullptr,
+      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<false>, blocks_for(total), (const G1A*)nullptr, (uint64_t)0,
              (const uint32_t*)nullptr, items, cur_off, (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg),
              total, dptr<G1J>(part));
     if (total == nseg) return dptr<G1J>(part);
@@ -135,7 +135,7 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
   }
   // bucket sums (mixed additions of the gathered affine bases)
-  G1J* buckets = seg_reduce(c, bases, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
+  G1J* buckets = seg_reduce(c, bases, n, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
   // per window: sum_d d B_d over chunks of buckets, then over the chunks
   const uint32_t chunks = (1u << bb) / kBucketChunk;
   DevBuf& chb = c->msm[13];
@@ -147,7 +147,7 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   DevBuf& wo = c->msm[14];
   wo.ensure((W + 1) * 4);
   HIPCK(hipMemcpyAsync(wo.p, woff.data(), (W + 1) * 4, hipMemcpyHostToDevice, c->stream));
-  G1J* ws = seg_reduce(c, nullptr, nullptr, dptr<G1J>(chb), dptr<uint32_t>(wo), W, 5);
+  G1J* ws = seg_reduce(c, nullptr, 0, nullptr, dptr<G1J>(chb), dptr<uint32_t>(wo), W, 5);
   std::vector<G1J> S(W);
   HIPCK(hipMemcpyAsync(S.data(), ws, W * sizeof(G1J), hipMemcpyDeviceToHost, c->stream));
   sync(c);

@@ -133,7 +133,10 @@ template <class F>
 __device__ __forceinline__ void d0m_load(const Fe* __restrict__ T, uint64_t Q, uint64_t j, Fe (&c)[4]) {
   if (j < Q) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = ld_fe(T, j + k * Q);
+    for (int k = 0; k < 4; ++k) {
+      ZK_DCHECK(j + k * Q < 4 * Q);
+      c[k] = ld_fe(T, j + k * Q);
+    }
   } else {  // past the end: zero points (every lane stays active for the transposed reads)
 #pragma unroll
     for (int k = 0; k < 4; ++k) c[k] = fe_zero<F>();
@@ -371,7 +374,10 @@ __device__ __forceinline__ Fe dm_finish(const int64_t (&W)[8], const Fe& x00) {
 // (ra, rb, rab); every lane folds its own element, wf[c] = the A fragments of the constants
 __device__ __forceinline__ void dm_load(const Fe* __restrict__ X, uint64_t i, uint64_t h4, Fe (&x)[4]) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) x[k] = ld_fe(X, i + k * h4);  // x00, x01, x10, x11
+  for (int k = 0; k < 4; ++k) {
+    ZK_DCHECK(i + k * h4 < 4 * h4);
+    x[k] = ld_fe(X, i + k * h4);  // x00, x01, x10, x11
+  }
 }
 template <class F>
 __device__ __forceinline__ Fe dm_fold(const Fe (&x)[4], const i32x4 (&wf)[3]) {
@@ -539,6 +545,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm(const Fe* __restrict__ A, 
       else if (ch + gridDim.x < nch)
         dm_load(X, (ch + gridDim.x) * kDMQuads + l, h4, in);
       z[k] = dm_fold<F>(cur, wf);
+      ZK_DCHECK(j + k * Q < 4 * Q);
       st_fold(X2, j + k * Q, z[k]);
     }
     dm_products<F>(z, sc, acc);
@@ -728,6 +735,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   uint64_t ch = blockIdx.x >> 1;
   Fe cn[2];
   if (ch < nch) {
+    ZK_DCHECK(ch * 32 + ql + (2 * w + 1) * O < 8 * O);
     cn[0] = ld_fe(T, ch * 32 + ql + (2 * w) * O);
     cn[1] = ld_fe(T, ch * 32 + ql + (2 * w + 1) * O);
   }
@@ -739,6 +747,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
       st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
     }
     if (ch + nb < nch) {  // the next chunk's corners, in flight during this chunk's products
+      ZK_DCHECK((ch + nb) * 32 + ql + (2 * w + 1) * O < 8 * O);
       cn[0] = ld_fe(T, (ch + nb) * 32 + ql + (2 * w) * O);
       cn[1] = ld_fe(T, (ch + nb) * 32 + ql + (2 * w + 1) * O);
     }
@@ -835,8 +844,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_dm3(const Fe* __restrict__ A,
     for (int k = 0; k < 4; ++k) {
       Fe x[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) x[c] = ld_fe(X, j + k * Q + c * h4);
+      for (int c = 0; c < 8; ++c) {
+        ZK_DCHECK(j + k * Q + c * h4 < 8 * h4);
+        x[c] = ld_fe(X, j + k * Q + c * h4);
+      }
       z[k] = dm3_fold<F>(x, wf);
+      ZK_DCHECK(j + k * Q < 4 * Q);
       st_fold(X2, j + k * Q, z[k]);
     }
     dm_products<F>(z, sc, acc);
@@ -912,7 +925,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     ch = ch < nch ? ch : 0;
     const uint64_t e = ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
 #pragma unroll
-    for (int k = 0; k < NI; ++k) x[k] = ld_fe(X, e + k * h8);
+    for (int k = 0; k < NI; ++k) {
+      ZK_DCHECK(e + k * h8 < 8 * h8);
+      x[k] = ld_fe(X, e + k * h8);
+    }
   };
   // Inputs two folds ahead for OCT 64, one for OCT 32 (one wave per SIMD: the
   // loads in flight are what hides HBM latency). The first ones (written by
@@ -924,7 +940,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     ch = ch < nch ? ch : 0;
     const uint64_t e = ch * 64 + l + (uint64_t)u * O;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = ld_fe(X, e + k * h8);
+    for (int k = 0; k < 8; ++k) {
+      ZK_DCHECK(e + k * h8 < 8 * h8);
+      x[k] = ld_fe(X, e + k * h8);
+    }
   };
   Fe nx[8], nx2[8];
   const bool early = (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
@@ -981,6 +1000,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       int64_t W[8];
       fold_words(a0, a1, W);
       const Fe z = dm_finish<F>(W, fe_zero<F>());
+      ZK_DCHECK(ch * 64 + l + (uint64_t)f * O < 8 * O);
       st_fold(X2, ch * 64 + l + (uint64_t)f * O, z);
       dm_row<F>(img[f][w][l], z);
     }
@@ -1021,6 +1041,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       in_at(f < 3 ? ch : ch + gridDim.x, f < 3 ? f + 1 : 0, nx);
       const uint32_t corner = 2 * f + hh;
       const Fe z = dm3_fold<F>(x, wf);
+      ZK_DCHECK(ch * 32 + ql + (uint64_t)corner * O < 8 * O);
       st_fold(X2, ch * 32 + ql + (uint64_t)corner * O, z);
       dm_row<F>(sc.img[buf][corner][w][ql], z);
     }

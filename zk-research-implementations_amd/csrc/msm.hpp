@@ -137,7 +137,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const Fe* __restrict__ 
   const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
   for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
     signed_digits(ld_fe(scalars, i), c, W, [&](uint32_t w, uint32_t key, uint32_t neg) {
-      E[atomicAdd(&cur[(w << C) + (key & ((1u << C) - 1u))], 1u)] = (i << (F + 1)) | ((uint64_t)neg << F) | (key >> C);
+      const uint32_t pos = atomicAdd(&cur[(w << C) + (key & ((1u << C) - 1u))], 1u);
+      ZK_DCHECK((uint64_t)pos < n * W);
+      E[pos] = (i << (F + 1)) | ((uint64_t)neg << F) | (key >> C);
     });
 }
 // grid = W 2^C blocks, one per coarse bin; cnt gets (W << b) + 1 offsets (b: bucket bits)
@@ -182,7 +184,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict
   __syncthreads();
   for (uint32_t e = start + t; e < end; e += kBlock) {
     const uint64_t x = E[e];
-    ord[atomicAdd(&h[(uint32_t)x & (nf - 1u)], 1u)] = (uint32_t)(x >> (F + 1)) | ((uint32_t)(x >> F) & 1u) << 31;
+    const uint32_t pos = atomicAdd(&h[(uint32_t)x & (nf - 1u)], 1u);
+    ZK_DCHECK(pos >= start && pos < end);
+    ord[pos] = (uint32_t)(x >> (F + 1)) | ((uint32_t)(x >> F) & 1u) << 31;
   }
 }
 
@@ -207,7 +211,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_task_owner(const uint32_t* __res
 }
 // GATHER: items are affine bases[order[j]]; else contiguous Jacobian points
 template <bool GATHER>
-__global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ bases, const uint32_t* __restrict__ order,
+__global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ bases, uint64_t nbases,
+                                                    const uint32_t* __restrict__ order,
                                                     const G1J* __restrict__ items, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ task_off,
                                                     const uint32_t* __restrict__ task_seg, uint32_t ntasks,
@@ -221,6 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
     G1XYZZ acc = g1x_inf();
     for (uint32_t j = a; j < b; ++j) {
       const uint32_t o = order[j];
+      ZK_DCHECK((o & 0x7fffffffu) < nbases);
       G1A p = bases[o & 0x7fffffffu];
       if (o >> 31) p.y = fq_neg(p.y);
       acc = g1x_add_mixed(acc, p);
@@ -254,6 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict_
   const G1J* B = buckets + ((uint64_t)w << c);
   G1J t = g1_inf(), u = g1_inf();
   for (uint32_t d = hi; d-- > lo;) {
+    ZK_DCHECK(bucket_slot(d, c) < (1u << c));
     t = g1_add(t, B[bucket_slot(d, c)]);
     if (d > lo) u = g1_add(u, t);
   }
@@ -286,6 +293,7 @@ __global__ __launch_bounds__(kBlock) void k_table20(const G1A* __restrict__ t16,
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < (uint64_t)kFB20W * kFB20; i += stride) {
     const uint32_t w = (uint32_t)(i >> 19), j = (uint32_t)i & (kFB20 - 1u), m = j ? j : kFB20;
     const uint32_t k = 20 * w / 16, o = 20 * w % 16;
+    ZK_DCHECK(k < 16 && ((uint64_t)(j ? j : kFB20) << o) < (1ull << 32));
     const uint64_t x = (uint64_t)m << o;  // < 2^32: its low and high 16 bits
     const G1A hi = k + 1 < 16 ? t16[(uint64_t)(k + 1) * kFB16 + (uint32_t)(x >> 16)] : G1A{fq_zero(), fq_zero()};
     out[i] = g1_add_mixed(g1_from_affine(t16[(uint64_t)k * kFB16 + (uint32_t)(x & 0xffffu)]), hi);
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_base20(const G1A* __restrict__
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
     G1XYZZ acc = g1x_inf();
     signed_digits(ld_fe(scalars, i), 20, kFB20W, [&](uint32_t w, uint32_t key, uint32_t neg) {
+      ZK_DCHECK(w < kFB20W && key < kFB20);
       G1A p = table[(uint64_t)w * kFB20 + key];
       if (neg) p.y = fq_neg(p.y);
       acc = g1x_add_mixed(acc, p);
@@ -316,6 +325,7 @@ __global__ __launch_bounds__(kBlock) void k_fixed_base8(const G1A* __restrict__ 
     G1XYZZ acc = g1x_inf();
     for (uint32_t w = 0; w < 32; ++w) {
       const uint32_t d = (fe_word(s, w >> 2) >> (8 * (w & 3))) & 0xffu;
+      ZK_DCHECK(w * 256 + d < 32u * 256u);
       if (d) acc = g1x_add_mixed(acc, t8[w * 256 + d]);
     }
     out[i] = g1x_to_jac(acc);
