@@ -240,6 +240,21 @@ ZK_HD G1XYZZ g1x_add_mixed(const G1XYZZ& p, const G1A& q) {  // madd-2008-s
   r.ZZZ = fq_mul(p.ZZZ, PPP);
   return r;
 }
+ZK_HD G1XYZZ g1x_add(const G1XYZZ& p, const G1XYZZ& q) {  // add-2008-s
+  if (fq_is_zero(q.ZZ)) return p;
+  if (fq_is_zero(p.ZZ)) return q;
+  const Fq U1 = fq_mul(p.X, q.ZZ), U2 = fq_mul(q.X, p.ZZ);
+  const Fq S1 = fq_mul(p.Y, q.ZZZ), S2 = fq_mul(q.Y, p.ZZZ);
+  const Fq P = fq_sub(U2, U1), R = fq_sub(S2, S1);
+  if (fq_is_zero(P)) return fq_is_zero(R) ? g1x_dbl(p) : g1x_inf();
+  const Fq PP = fq_sqr(P), PPP = fq_mul(P, PP), Q = fq_mul(U1, PP);
+  G1XYZZ r;
+  r.X = fq_sub(fq_sub(fq_sqr(R), PPP), fq_dbl(Q));
+  r.Y = fq_sub(fq_mul(R, fq_sub(Q, r.X)), fq_mul(S1, PPP));
+  r.ZZ = fq_mul(fq_mul(p.ZZ, q.ZZ), PP);
+  r.ZZZ = fq_mul(fq_mul(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
 // Jacobian with Z' = ZZ ZZZ (= Z^5 for Z^2 = ZZ): X' = X ZZ^4, Y' = Y ZZZ^4
 ZK_HD G1J g1x_to_jac(const G1XYZZ& p) {
   if (fq_is_zero(p.ZZ)) return g1_inf();

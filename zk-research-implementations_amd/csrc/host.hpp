@@ -242,7 +242,8 @@ struct zk_ctx {
   void* user = nullptr;
   ncclComm_t nccl = nullptr;
   // KZG / MSM scratch (grow-only) and the cached fixed-base table of G1
-  DevBuf msm[17];
+  DevBuf msm[19];
+  bool msm_balanced = true;  // ZK_MSM_BALANCED: bucket sums in equal tasks across bucket boundaries (kzg.hip)
   DevBuf scan_tmp[4];
   DevBuf g1_table;
   DevBuf g1_table16;  // 16-bit windows (100 MB), built on the device from g1_table

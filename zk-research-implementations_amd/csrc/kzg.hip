@@ -60,9 +60,10 @@ uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + zk
 // Level 0 reads affine bases[order[j]] (order != null) or Jacobian items0[j].
 // Uses c->msm[pool .. pool+4]; returns a device pointer to nseg sums.
 G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* order, const G1J* items0,
-                const uint32_t* off, uint64_t nseg, int pool) {
+                const uint32_t* off, uint64_t nseg, int pool, const zk::G1XYZZ* xitems0 = nullptr) {
   const G1J* items = items0;
   bool gather = order != nullptr;
+  bool xyzz = xitems0 != nullptr;  // level 0 sums XYZZ partials (k_seg_sum_xyzz)
   const uint32_t* cur_off = off;
   int flip = 0;
   for (int level = 0;; ++level) {
@@ -82,7 +83,10 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
     launch(c, ZK_K_MSM, 4.0 * total, 0, zk::k_seg_task_owner, blocks_for(nseg), (const uint32_t*)to, nseg, total,
            dptr<uint32_t>(tseg));
     part.ensure((size_t)total * sizeof(G1J));
-    if (gather)
+    if (xyzz)
+      launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum_xyzz, blocks_for(total), xitems0, cur_off, (const uint32_t*)to,
+             (const uint32_t*)dptr<uint32_t>(tseg), total, dptr<G1J>(part));
+    else if (gather)
       launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<true>, blocks_for(total), bases, nbases, order, (const G1J*)nullptr, cur_off,
              (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg), total, dptr<G1J>(part));
     else
@@ -93,6 +97,7 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
     items = dptr<G1J>(part);
     cur_off = to;
     gather = false;
+    xyzz = false;
     flip ^= 1;
   }
 }
@@ -134,8 +139,34 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
     launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), bb, NB,
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
   }
-  // bucket sums (mixed additions of the gathered affine bases)
-  G1J* buckets = seg_reduce(c, bases, n, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
+  // bucket sums (mixed additions of the gathered affine bases): balanced tasks
+  // of kBalTask entries across bucket boundaries, one XYZZ partial per bucket
+  // a task touches, then each bucket's partials summed (msm.hpp "balanced")
+  G1J* buckets;
+  if (c->msm_balanced) {
+    DevBuf& bc = c->msm[17];
+    bc.ensure((nb + 1) * 4);
+    uint32_t* pbal = dptr<uint32_t>(bc);
+    launch(c, ZK_K_MSM, 12.0 * nb, 0, k_bal_counts, blocks_for(nb), (const uint32_t*)dptr<uint32_t>(cnt), nb, pbal);
+    HIPCK(hipMemsetAsync(pbal + nb, 0, 4, c->stream));
+    scan_u32(c, pbal, nb + 1);
+    uint32_t sizes[2] = {0, 0};  // entries, partials
+    HIPCK(hipMemcpyAsync(&sizes[0], dptr<uint32_t>(cnt) + nb, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipMemcpyAsync(&sizes[1], pbal + nb, 4, hipMemcpyDeviceToHost, c->stream));
+    sync(c);
+    DevBuf& pb = c->msm[18];
+    pb.ensure(std::max<uint64_t>(1, sizes[1]) * sizeof(G1XYZZ));
+    G1XYZZ* parts = dptr<G1XYZZ>(pb);
+    launch(c, ZK_K_MSM, 0, 0, k_bal_empty, blocks_for(nb), (const uint32_t*)dptr<uint32_t>(cnt), nb,
+           (const uint32_t*)pbal, parts);
+    const uint64_t ntask = ((uint64_t)sizes[0] + kBalTask - 1) / kBalTask;
+    if (ntask)
+      launch(c, ZK_K_MSM, 0, 0, k_seg_sum_bal, blocks_for(ntask), bases, n, (const uint32_t*)dptr<uint32_t>(ord),
+             (const uint32_t*)dptr<uint32_t>(cnt), nb, sizes[0], (const uint32_t*)pbal, (uint64_t)sizes[1], parts);
+    buckets = seg_reduce(c, nullptr, 0, nullptr, nullptr, pbal, nb, 0, parts);
+  } else {
+    buckets = seg_reduce(c, bases, n, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
+  }
   // per window: sum_d d B_d over chunks of buckets, then over the chunks
   const uint32_t chunks = (1u << bb) / kBucketChunk;
   DevBuf& chb = c->msm[13];

@@ -239,6 +239,95 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
   }
 }
 
+// ---- balanced bucket sums (round 5) ---------------------------------------------------
+// The sorted entries (point order, bucket slot order) cut into equal tasks of
+// kBalTask consecutive entries, one per thread, regardless of bucket
+// boundaries — k_seg_sum<true> gave each bucket its own tasks of <= 32, so a
+// wave ran 32 iterations for tasks averaging ~22 (random scalars: ~32 entries
+// per bucket), ~70 % of its lanes busy. A thread emits one XYZZ partial per
+// bucket slot its task touches (divergent stores only: no arithmetic under a
+// branch) at pbal[s] + (task - first task of s); k_bal_empty writes the
+// infinity of every empty slot; k_seg_sum_xyzz then sums each slot's partials
+// (usually 1 or 2) to its Jacobian bucket sum. Group arithmetic is exact, so
+// the bucket sums are the same group elements as before.
+#ifndef ZK_BAL_TASK
+#define ZK_BAL_TASK 32
+#endif
+constexpr uint32_t kBalTask = ZK_BAL_TASK;
+// partials of slot s: one per task its entries touch (an empty slot: 1, its infinity)
+__global__ __launch_bounds__(kBlock) void k_bal_counts(const uint32_t* __restrict__ cnt, uint64_t nseg,
+                                                       uint32_t* __restrict__ counts) {
+  const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (s >= nseg) return;
+  const uint32_t a = cnt[s], b = cnt[s + 1];
+  counts[s] = a == b ? 1u : (b - 1) / kBalTask - a / kBalTask + 1;
+}
+__global__ __launch_bounds__(kBlock) void k_bal_empty(const uint32_t* __restrict__ cnt, uint64_t nseg,
+                                                      const uint32_t* __restrict__ pbal, G1XYZZ* __restrict__ out) {
+  const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (s >= nseg) return;
+  if (cnt[s] == cnt[s + 1]) out[pbal[s]] = g1x_inf();
+}
+__global__ __launch_bounds__(kBlock) void k_seg_sum_bal(const G1A* __restrict__ bases, uint64_t nbases,
+                                                        const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ cnt, uint64_t nseg, uint32_t total,
+                                                        const uint32_t* __restrict__ pbal, uint64_t npart,
+                                                        G1XYZZ* __restrict__ out) {
+  const uint64_t task = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t lo = task * kBalTask;
+  if (lo >= total) return;
+  const uint32_t hi = (uint32_t)(lo + kBalTask < total ? lo + kBalTask : total);
+  // the slot holding entry lo: the first s with cnt[s + 1] > lo
+  uint64_t L = 0, H = nseg - 1;
+  while (L < H) {
+    const uint64_t M = (L + H) >> 1;
+    if (cnt[M + 1] > lo) H = M;
+    else L = M + 1;
+  }
+  uint64_t s = L;
+  uint32_t a = cnt[s], b = cnt[s + 1];
+  auto emit = [&](const G1XYZZ& acc) {
+    const uint64_t at = pbal[s] + (task - a / kBalTask);
+    ZK_DCHECK(at < npart && at < pbal[s + 1]);
+    out[at] = acc;
+  };
+  G1XYZZ acc = g1x_inf();
+  for (uint32_t j = (uint32_t)lo; j < hi; ++j) {
+    if (j == b) {  // slot s ends here: its partial, then the next non-empty slot (empty ones: k_bal_empty)
+      emit(acc);
+      do {
+        ++s;
+        a = cnt[s];
+        b = cnt[s + 1];
+      } while (a == b);
+      acc = g1x_inf();
+    }
+    const uint32_t o = order[j];
+    ZK_DCHECK((o & 0x7fffffffu) < nbases);
+    G1A p = bases[o & 0x7fffffffu];
+    if (o >> 31) p.y = fq_neg(p.y);
+    acc = g1x_add_mixed(acc, p);
+  }
+  emit(acc);
+}
+// sum each slot's XYZZ partials [pbal[s], pbal[s + 1]) -> its Jacobian bucket sum
+// (segments longer than kXyzzTask — skewed scalars — leave partial sums for
+// seg_reduce's next levels: out gets one item per task, task_off as k_seg_sum)
+constexpr uint32_t kXyzzTask = kSegTask;  // (task counts from k_seg_task_counts)
+__global__ __launch_bounds__(kBlock) void k_seg_sum_xyzz(const G1XYZZ* __restrict__ items, const uint32_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ task_off,
+                                                         const uint32_t* __restrict__ task_seg, uint32_t ntasks,
+                                                         G1J* __restrict__ out) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= ntasks) return;
+  const uint32_t s = task_seg[t], k = t - task_off[s];
+  const uint32_t a = off[s] + k * kXyzzTask, e = off[s + 1];
+  const uint32_t b = a + kXyzzTask < e ? a + kXyzzTask : e;
+  G1XYZZ acc = g1x_inf();
+  for (uint32_t j = a; j < b; ++j) acc = g1x_add(acc, items[j]);
+  out[t] = g1x_to_jac(acc);
+}
+
 // ---- window reduction -----------------------------------------------------------
 // For window w, chunk j of buckets d in [lo, hi): sum_d d B_d = u + lo * T with
 // T = sum B_d, u = sum (d - lo) B_d (running sum from the top), at
