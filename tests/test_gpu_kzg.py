@@ -250,3 +250,29 @@ def test_setup_tables_agree_across_threshold(ctx):
         ctx2.close()
     k16.close()
     k15.close()
+
+
+@pytest.mark.parametrize("balanced", ["0", "1"])
+def test_bucket_sum_paths_agree(monkeypatch, balanced):
+    """Both bucket-sum paths (ZK_MSM_BALANCED=1, the default: equal tasks of
+    kBalTask entries across bucket boundaries with XYZZ partials; 0: one task
+    per <= 32 entries of a bucket) give the oracle's MSM on random scalars, on
+    buckets split over many tasks (one base 20 000 times: equal partials meet
+    in the XYZZ doubling), and on cancelling pairs."""
+    import zk_amd
+
+    monkeypatch.setenv("ZK_MSM_BALANCED", balanced)
+    ctx = zk_amd.Context(0)
+    try:
+        rng = random.Random(31)
+        ks = [rng.randrange(1, 1000) for _ in range(9)]
+        pts = [ko.mul(k, ko.G1) for k in ks]
+        n = 3 * 16384 + 5
+        scalars = [rng.randrange(R) for _ in range(n)]
+        bases = [pts[i % len(ks)] for i in range(n)]
+        want = sum(s * ks[i % len(ks)] for i, s in enumerate(scalars)) % R
+        assert msm_g1(bases, scalars, ctx) == ko.mul(want, ko.G1)
+        assert msm_g1([pts[0]] * 20000, [3] * 20000, ctx) == ko.mul(60000 * ks[0], ko.G1)
+        assert msm_g1([pts[2], pts[2], pts[3]], [5, R - 5, 0], ctx) is None
+    finally:
+        ctx.close()

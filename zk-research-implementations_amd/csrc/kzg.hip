@@ -60,7 +60,8 @@ uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + zk
 // Level 0 reads affine bases[order[j]] (order != null) or Jacobian items0[j].
 // Uses c->msm[pool .. pool+4]; returns a device pointer to nseg sums.
 G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* order, const G1J* items0,
-                const uint32_t* off, uint64_t nseg, int pool, const zk::G1XYZZ* xitems0 = nullptr) {
+                const uint32_t* off, uint64_t nseg, int pool, const zk::G1XYZZ* xitems0 = nullptr,
+                uint32_t task = zk::kSegTask) {
   const G1J* items = items0;
   bool gather = order != nullptr;
   bool xyzz = xitems0 != nullptr;  // level 0 sums XYZZ partials (k_seg_sum_xyzz)
@@ -73,7 +74,7 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
     DevBuf& part = c->msm[pool + 3 + flip];
     toff.ensure((nseg + 1) * 4);
     uint32_t* to = dptr<uint32_t>(toff);
-    launch(c, ZK_K_MSM, 12.0 * nseg, 0, zk::k_seg_task_counts, blocks_for(nseg), cur_off, nseg, to);
+    launch(c, ZK_K_MSM, 12.0 * nseg, 0, zk::k_seg_task_counts, blocks_for(nseg), cur_off, nseg, task, to);
     HIPCK(hipMemsetAsync(to + nseg, 0, 4, c->stream));
     scan_u32(c, to, nseg + 1);
     uint32_t total = 0;
@@ -85,14 +86,14 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
     part.ensure((size_t)total * sizeof(G1J));
     if (xyzz)
       launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum_xyzz, blocks_for(total), xitems0, cur_off, (const uint32_t*)to,
-             (const uint32_t*)dptr<uint32_t>(tseg), total, dptr<G1J>(part));
+             (const uint32_t*)dptr<uint32_t>(tseg), total, task, dptr<G1J>(part));
     else if (gather)
       launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<true>, blocks_for(total), bases, nbases, order, (const G1J*)nullptr, cur_off,
-             (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg), total, dptr<G1J>(part));
+             (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg), total, task, dptr<G1J>(part));
     else
       launch(c, ZK_K_MSM, 0, 0, zk::k_seg_sum<false>, blocks_for(total), (const G1A*)nullptr, (uint64_t)0,
              (const uint32_t*)nullptr, items, cur_off, (const uint32_t*)to, (const uint32_t*)dptr<uint32_t>(tseg),
-             total, dptr<G1J>(part));
+             total, task, dptr<G1J>(part));
     if (total == nseg) return dptr<G1J>(part);
     items = dptr<G1J>(part);
     cur_off = to;
@@ -178,7 +179,8 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   DevBuf& wo = c->msm[14];
   wo.ensure((W + 1) * 4);
   HIPCK(hipMemcpyAsync(wo.p, woff.data(), (W + 1) * 4, hipMemcpyHostToDevice, c->stream));
-  G1J* ws = seg_reduce(c, nullptr, 0, nullptr, dptr<G1J>(chb), dptr<uint32_t>(wo), W, 5);
+  // (few, long segments: short tasks keep the levels parallel instead of 32 serial additions per thread)
+  G1J* ws = seg_reduce(c, nullptr, 0, nullptr, dptr<G1J>(chb), dptr<uint32_t>(wo), W, 5, nullptr, c->msm_win_task);
   std::vector<G1J> S(W);
   HIPCK(hipMemcpyAsync(S.data(), ws, W * sizeof(G1J), hipMemcpyDeviceToHost, c->stream));
   sync(c);

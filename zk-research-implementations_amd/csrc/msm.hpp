@@ -19,7 +19,11 @@
 namespace zk {
 
 constexpr uint32_t kSegTask = 32;    // points summed by one thread per reduction level
-constexpr uint32_t kBucketChunk = 16;  // buckets per thread in the window reduction
+#ifndef ZK_BUCKET_CHUNK
+#define ZK_BUCKET_CHUNK 32
+#endif
+constexpr uint32_t kBucketChunk = ZK_BUCKET_CHUNK;  // buckets per thread in the window reduction (<= 32: c >= 6)
+static_assert(kBucketChunk <= 32, "the smallest window (c = 6) has 32 buckets");
 
 __device__ __forceinline__ Fq ld_fq(const Fq* p, uint64_t i) { return p[i]; }
 
@@ -195,11 +199,11 @@ __global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict
 // (at least 1, so empty segments yield infinity); task t of segment s sums
 // items [off[s] + k T, min(off[s+1], off[s] + (k+1) T)).
 __global__ __launch_bounds__(kBlock) void k_seg_task_counts(const uint32_t* __restrict__ off, uint64_t nseg,
-                                                            uint32_t* __restrict__ tasks) {
+                                                            uint32_t task, uint32_t* __restrict__ tasks) {
   const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (s >= nseg) return;
   const uint32_t len = off[s + 1] - off[s];
-  tasks[s] = len ? (len + kSegTask - 1) / kSegTask : 1u;
+  tasks[s] = len ? (len + task - 1) / task : 1u;
 }
 // task_seg[task_off[s] + k] = s
 __global__ __launch_bounds__(kBlock) void k_seg_task_owner(const uint32_t* __restrict__ task_off, uint64_t nseg,
@@ -216,12 +220,12 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
                                                     const G1J* __restrict__ items, const uint32_t* __restrict__ off,
                                                     const uint32_t* __restrict__ task_off,
                                                     const uint32_t* __restrict__ task_seg, uint32_t ntasks,
-                                                    G1J* __restrict__ out) {
+                                                    uint32_t task, G1J* __restrict__ out) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= ntasks) return;
   const uint32_t s = task_seg[t], k = t - task_off[s];
-  const uint32_t a = off[s] + k * kSegTask, e = off[s + 1];
-  const uint32_t b = a + kSegTask < e ? a + kSegTask : e;
+  const uint32_t a = off[s] + k * task, e = off[s + 1];
+  const uint32_t b = a + task < e ? a + task : e;
   if constexpr (GATHER) {  // XYZZ accumulator over affine points (ec.hpp); order bit 31: negative digit
     G1XYZZ acc = g1x_inf();
     for (uint32_t j = a; j < b; ++j) {
@@ -251,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
 // (usually 1 or 2) to its Jacobian bucket sum. Group arithmetic is exact, so
 // the bucket sums are the same group elements as before.
 #ifndef ZK_BAL_TASK
-#define ZK_BAL_TASK 32
+#define ZK_BAL_TASK 64
 #endif
 constexpr uint32_t kBalTask = ZK_BAL_TASK;
 // partials of slot s: one per task its entries touch (an empty slot: 1, its infinity)
@@ -311,18 +315,17 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum_bal(const G1A* __restrict__ 
   emit(acc);
 }
 // sum each slot's XYZZ partials [pbal[s], pbal[s + 1]) -> its Jacobian bucket sum
-// (segments longer than kXyzzTask — skewed scalars — leave partial sums for
+// (segments longer than a task — skewed scalars — leave partial sums for
 // seg_reduce's next levels: out gets one item per task, task_off as k_seg_sum)
-constexpr uint32_t kXyzzTask = kSegTask;  // (task counts from k_seg_task_counts)
 __global__ __launch_bounds__(kBlock) void k_seg_sum_xyzz(const G1XYZZ* __restrict__ items, const uint32_t* __restrict__ off,
                                                          const uint32_t* __restrict__ task_off,
                                                          const uint32_t* __restrict__ task_seg, uint32_t ntasks,
-                                                         G1J* __restrict__ out) {
+                                                         uint32_t task, G1J* __restrict__ out) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= ntasks) return;
   const uint32_t s = task_seg[t], k = t - task_off[s];
-  const uint32_t a = off[s] + k * kXyzzTask, e = off[s + 1];
-  const uint32_t b = a + kXyzzTask < e ? a + kXyzzTask : e;
+  const uint32_t a = off[s] + k * task, e = off[s + 1];
+  const uint32_t b = a + task < e ? a + task : e;
   G1XYZZ acc = g1x_inf();
   for (uint32_t j = a; j < b; ++j) acc = g1x_add(acc, items[j]);
   out[t] = g1x_to_jac(acc);
