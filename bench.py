@@ -404,6 +404,39 @@ def circuit_bench(ctx, field: int, log_inputs: int = 12, reps: int = 7) -> dict:
     }
 
 
+def circuit_kzg_bench(ctx, log_inputs: int = 14, reps: int = 5) -> dict:
+    """gkr::prove WITH the input layer's KZG step (gkr_protocol.rs:92-118;
+    zk_gkr_circuit_prove_kzg) over BLS12-381 Fr at the largest circuit the
+    layered prover takes (2^14 inputs): circuit GKR + KZG setup over 14
+    variables + commit + two get_proofs; gkr::verify (with both KZG pairings
+    checks, no inputs) must accept it."""
+    import random
+
+    import zk_amd
+    from zk_amd.gkr import Circuit, Operation, prove, verify
+    from zk_amd.elems import as_limbs
+
+    field = 2
+    rng = random.Random(14)
+    structure = [[rng.choice((Operation.Add, Operation.Mul)) for _ in range(1 << (log_inputs - 1 - i))]
+                 for i in range(log_inputs)]
+    p = zk_amd.modulus(field)
+    x = as_limbs([rng.randrange(p) for _ in range(1 << log_inputs)])
+    taus = [rng.randrange(p) for _ in range(log_inputs)]
+    circ = Circuit(structure, field)
+    proof = prove(circ, x, ctx, taus=taus)  # warm-up (and the setup's tables)
+    ok = verify(proof, circ)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        prove(circ, x, ctx, taus=taus)
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    return {"workload": f"gkr::prove with the input layer's KZG (setup, commit, 2 get_proofs over {log_inputs} "
+                        f"variables), random {log_inputs}-layer circuit, {1 << log_inputs} inputs, BLS12-381 Fr",
+            "ms_median": times[len(times) // 2] * 1e3, "reps": reps, "verified": bool(ok)}
+
+
 def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
     """BASELINE config 5: the 24-variable GKR sum-check over BLS12-381 Fr, and
     the KZG commitment of a 24-variable MLE over BLS12-381
@@ -453,8 +486,31 @@ def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
         check(lib().zk_dev_kzg_commit(ctx.h, k.h, evals.ptr, ptr(out)))
         ts.append(time.perf_counter() - t0)
     commit_ms = sorted(ts)[reps // 2] * 1e3
-    k.close()
     commit_check = kzg_commit_check(nvars, out)
+    # KZG::get_proof (kzg.rs:59-95) of the same MLE at a random point: nvars
+    # quotient commitments (MSMs of 2^(nvars-1) .. 1 points) from host memory
+    # (the ABI takes host evaluations: a 512 MiB upload is inside the time),
+    # checked by KZG::verify's pairings (host, kzg.rs:97-129)
+    from zk_amd.context import REPR_CANONICAL
+    from zk_amd.kzg import _points
+
+    host = evals.download()  # canonical limbs
+    point = [rng.randrange(zk_amd.modulus(field)) for _ in range(nvars)]
+    pt = as_limbs(point)
+    v = np.zeros((1, 4), np.uint64)
+    check(lib().zk_mle_evaluate(ctx.h, field, REPR_CANONICAL, ptr(host), nvars, ptr(pt), nvars, ptr(v)))
+    prf = np.zeros((nvars, 12), np.uint64)
+    t0 = time.perf_counter()
+    check(lib().zk_kzg_get_proof(ctx.h, k.h, REPR_CANONICAL, ptr(host), ptr(v), ptr(pt), ptr(prf)))
+    proof_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    proof_ok = KZG.verify(_points(out)[0], int(sum(int(v[0, i]) << (64 * i) for i in range(4))), _points(prf), point,
+                          k.g2_taus)
+    verify_ms = (time.perf_counter() - t0) * 1e3
+    if not proof_ok:
+        raise SystemExit("KZG get_proof at full size did not verify")
+    k.close()
+    del host
     # a second setup (other taus) on the same context: its fixed-base table and
     # scratch buffers already exist, so this is the steady-state cost of a setup
     t0 = time.perf_counter()
@@ -472,6 +528,11 @@ def config5_bench(ctx, nvars: int = 24, reps: int = 3) -> dict:
         "kzg_commit_ms": commit_ms,
         "msm_points_per_s": n / (commit_ms / 1e3),
         "commit_check": commit_check,
+        "kzg_get_proof_ms": proof_ms,
+        "kzg_get_proof_note": f"{nvars} quotient commitments (MSMs of 2^{nvars - 1} .. 1 points) + folds, from host "
+                              "evaluations (512 MiB upload inside the time); verified by KZG::verify's pairings",
+        "kzg_get_proof_verified": bool(proof_ok),
+        "kzg_verify_host_ms": verify_ms,
         "note": "the reference commits with a naive sum of 2^24 full scalar multiplications (kzg.rs:131-144)",
     }
 
@@ -888,6 +949,7 @@ def main() -> None:
             out["gkr_circuit"] = circuit_bench(ctx, field)
         if not args.no_config5 and world == 1:
             out["config5_bls12_381"] = config5_bench(ctx)
+            out["gkr_circuit_kzg"] = circuit_kzg_bench(ctx)
         if not args.no_plain and world == 1:
             out["config1_12var_prove"] = config1_bench(ctx, field)
             out["plain_sumcheck"] = [plain_bench(ctx, field, nv) for nv in (20, 24)]

@@ -199,3 +199,26 @@ def test_input_kzg_accepts_limb_array_inputs(ctx):
     a = prove(circ, inputs, ctx, taus=[5, 2, 3])
     b = prove(circ, as_limbs(inputs), ctx, taus=[5, 2, 3])
     assert a == b
+
+
+def test_circuit_with_input_kzg_at_scale(ctx):
+    """gkr::prove with the input layer's KZG step on a random 10-layer circuit
+    (1 024 inputs, BLS12-381 Fr): gkr::verify — the layer sum-checks and both
+    KZG pairing checks, without the inputs — accepts it, and rejects a proof
+    whose opened evaluation was changed."""
+    import dataclasses
+    import random
+
+    rng = random.Random(1024)
+    log_in = 10
+    structure = [[rng.choice((A, M)) for _ in range(1 << (log_in - 1 - i))] for i in range(log_in)]
+    p = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    inputs = [rng.randrange(p) for _ in range(1 << log_in)]
+    taus = [rng.randrange(p) for _ in range(log_in)]
+    circ = Circuit([[OPS[o] for o in layer] for layer in structure], 2)
+    got = prove(circ, inputs, ctx, taus=taus)
+    assert verify(got, circ)
+    assert verify(got, circ, inputs)
+    kp = got.input_proof
+    bad = dataclasses.replace(kp, opened_evals=(kp.opened_evals[0], (kp.opened_evals[1] + 1) % p))
+    assert not verify(dataclasses.replace(got, input_proof=bad), circ)

@@ -276,3 +276,23 @@ def test_bucket_sum_paths_agree(monkeypatch, balanced):
         assert msm_g1([pts[2], pts[2], pts[3]], [5, R - 5, 0], ctx) is None
     finally:
         ctx.close()
+
+
+def test_get_proof_large_window_verifies(ctx):
+    """KZG::get_proof (kzg.rs:59-95) at 20 variables — quotient MSMs of 2^19
+    .. 1 points, the large signed windows (c up to 16) and the balanced bucket
+    sums — accepted by KZG::verify's pairings (kzg.rs:97-129) and rejected with
+    a wrong opened value or a swapped proof."""
+    rng = random.Random(20)
+    n = 20
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    point = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    c = k.commit(evals)
+    v = k.open(point, evals)
+    proof = k.get_proof(v, point, evals)
+    assert KZG.verify(c, v, proof, point, k.g2_taus)
+    assert not KZG.verify(c, (v + 1) % R, proof, point, k.g2_taus)
+    assert not KZG.verify(c, v, proof[1:] + proof[:1], point, k.g2_taus)
+    k.close()
