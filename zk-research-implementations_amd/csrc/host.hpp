@@ -244,7 +244,7 @@ struct zk_ctx {
   // KZG / MSM scratch (grow-only) and the cached fixed-base table of G1
   DevBuf msm[19];
   bool msm_balanced = true;  // ZK_MSM_BALANCED: bucket sums in equal tasks across bucket boundaries (kzg.hip)
-  uint32_t msm_win_task = 8;  // ZK_MSM_WIN_TASK: points per task in the window sums' segmented reduction
+  uint32_t msm_win_task = 4;  // ZK_MSM_WIN_TASK: points per task in the window sums' segmented reduction
   DevBuf scan_tmp[4];
   DevBuf g1_table;
   DevBuf g1_table16;  // 16-bit windows (100 MB), built on the device from g1_table

@@ -1,6 +1,8 @@
 // Multilinear KZG over BLS12-381 G1: host driver and C ABI.
+#include <array>
 #include <map>
 #include <mutex>
+#include <thread>
 
 #include "host.hpp"
 #include "msm.hpp"
@@ -103,6 +105,11 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
   }
 }
 
+// a small MSM's time is one thread's serial chain of group additions: the
+// per-thread work of the bucket and window sums shrinks until at least this
+// many threads run (2 waves per SIMD of a 256-CU MI355X)
+constexpr uint64_t kMsmMinThreads = 1u << 17;
+
 // sum_i scalars[i] * bases[i]; scalars canonical Fr (device), bases affine Montgomery (device)
 G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   using namespace zk;
@@ -148,7 +155,11 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
     DevBuf& bc = c->msm[17];
     bc.ensure((nb + 1) * 4);
     uint32_t* pbal = dptr<uint32_t>(bc);
-    launch(c, ZK_K_MSM, 12.0 * nb, 0, k_bal_counts, blocks_for(nb), (const uint32_t*)dptr<uint32_t>(cnt), nb, pbal);
+    // entries per thread: kBalTaskMax unless that leaves fewer than ~2 waves per SIMD
+    uint32_t tsize = kBalTaskMax;
+    while (tsize > 4 && (uint64_t)n * W / tsize < kMsmMinThreads) tsize >>= 1;
+    launch(c, ZK_K_MSM, 12.0 * nb, 0, k_bal_counts, blocks_for(nb), (const uint32_t*)dptr<uint32_t>(cnt), nb, tsize,
+           pbal);
     HIPCK(hipMemsetAsync(pbal + nb, 0, 4, c->stream));
     scan_u32(c, pbal, nb + 1);
     uint32_t sizes[2] = {0, 0};  // entries, partials
@@ -160,19 +171,24 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
     G1XYZZ* parts = dptr<G1XYZZ>(pb);
     launch(c, ZK_K_MSM, 0, 0, k_bal_empty, blocks_for(nb), (const uint32_t*)dptr<uint32_t>(cnt), nb,
            (const uint32_t*)pbal, parts);
-    const uint64_t ntask = ((uint64_t)sizes[0] + kBalTask - 1) / kBalTask;
+    const uint64_t ntask = ((uint64_t)sizes[0] + tsize - 1) / tsize;
     if (ntask)
       launch(c, ZK_K_MSM, 0, 0, k_seg_sum_bal, blocks_for(ntask), bases, n, (const uint32_t*)dptr<uint32_t>(ord),
-             (const uint32_t*)dptr<uint32_t>(cnt), nb, sizes[0], (const uint32_t*)pbal, (uint64_t)sizes[1], parts);
-    buckets = seg_reduce(c, nullptr, 0, nullptr, nullptr, pbal, nb, 0, parts);
+             (const uint32_t*)dptr<uint32_t>(cnt), nb, sizes[0], tsize, (const uint32_t*)pbal, (uint64_t)sizes[1],
+             parts);
+    uint32_t ptask = kSegTask;  // partials per thread: fewer for small MSMs (serial chains)
+    while (ptask > 2 && sizes[1] / ptask < kMsmMinThreads) ptask >>= 1;
+    buckets = seg_reduce(c, nullptr, 0, nullptr, nullptr, pbal, nb, 0, parts, ptask);
   } else {
     buckets = seg_reduce(c, bases, n, dptr<uint32_t>(ord), nullptr, dptr<uint32_t>(cnt), nb, 0);
   }
   // per window: sum_d d B_d over chunks of buckets, then over the chunks
-  const uint32_t chunks = (1u << bb) / kBucketChunk;
+  uint32_t bchunk = kBucketChunkMax;  // buckets per thread: fewer when the windows are small (thread count)
+  while (bchunk > 1 && ((uint64_t)W << bb) / bchunk < kMsmMinThreads) bchunk >>= 1;
+  const uint32_t chunks = (1u << bb) / bchunk;
   DevBuf& chb = c->msm[13];
   chb.ensure((size_t)W * (chunks + 1) * sizeof(G1J));
-  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * (chunks + 1)), (const G1J*)buckets, bb, W,
+  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * (chunks + 1)), (const G1J*)buckets, bb, W, bchunk,
          dptr<G1J>(chb));
   std::vector<uint32_t> woff(W + 1);
   for (uint32_t w = 0; w <= W; ++w) woff[w] = w * (chunks + 1);
@@ -251,7 +267,7 @@ const G1A* g1_fixed_table16(zk_ctx* c) {
   launch(c, ZK_K_MSM, 0, 0, k_table16, grid_for(c, n, k_table16), t8, dptr<G1J>(jac.b));
   c->g1_table16.ensure(n * sizeof(G1A));
   launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
-         (const G1J*)dptr<G1J>(jac.b), n, dptr<G1A>(c->g1_table16));
+         (const G1J*)dptr<G1J>(jac.b), n, kBatchNorm, dptr<G1A>(c->g1_table16));
   sync(c);
   return dptr<G1A>(c->g1_table16);
 }
@@ -285,7 +301,7 @@ const G1A* g1_fixed_table20(zk_ctx* c) {
   t20.ensure(n * sizeof(G1A));
   try {
     launch(c, ZK_K_MSM, 240.0 * n, 0, k_batch_normalize, blocks_for((n + kBatchNorm - 1) / kBatchNorm),
-           (const G1J*)dptr<G1J>(jac.b), n, dptr<G1A>(t20));
+           (const G1J*)dptr<G1J>(jac.b), n, kBatchNorm, dptr<G1A>(t20));
     sync(c);
   } catch (...) {
     t20.release();
@@ -452,14 +468,21 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
              (const Fe*)sc.p, N, J + (N - 1));
     // G2 half of run_trusted_setup (:43-46): tau_i * G2, on the host (nvars
     // scalar multiplications) while the basis kernels run
+    // (split over up to 8 host threads; the scalars are converted and checked
+    // on this thread first, so nothing below can throw)
     {
       const zk::G2J g2 = zk::g2_from_affine(zk::g2_generator());
+      std::vector<std::array<uint32_t, 8>> tc(nvars);
+      for (uint32_t i = 0; i < nvars; ++i) fr_canon(repr, taus[i], tc[i].data());
       k->g2_taus.resize(nvars);
-      for (uint32_t i = 0; i < nvars; ++i) {
-        uint32_t t[8];
-        fr_canon(repr, taus[i], t);
-        k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, t));
-      }
+      const uint32_t nth = std::min<uint32_t>(nvars, 8);
+      auto work = [&](uint32_t w) {
+        for (uint32_t i = w; i < nvars; i += nth) k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, tc[i].data()));
+      };
+      std::vector<std::thread> pool;
+      for (uint32_t w = 1; w < nth; ++w) pool.emplace_back(work, w);
+      work(0);
+      for (auto& th : pool) th.join();
     }
     // suffix bases L^(v)_j = L^(v+1)_j + L^(v+1)_(2^v + j) (eq sums to 1 over the
     // dropped variable), Jacobian, then ONE batch normalisation of all levels:
@@ -470,8 +493,10 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
              n, J + (n - 1));
     }
     k->basis.ensure(total * sizeof(G1A));
-    launch(c, ZK_K_MSM, 240.0 * total, 0, zk::k_batch_normalize, blocks_for((total + zk::kBatchNorm - 1) / zk::kBatchNorm),
-           (const G1J*)J, total, dptr<G1A>(k->basis));
+    uint32_t nbatch = zk::kBatchNorm;  // (points per inversion: fewer for small setups, whose time is the chain)
+    while (nbatch > 1 && total / nbatch < kMsmMinThreads) nbatch >>= 1;
+    launch(c, ZK_K_MSM, 240.0 * total, 0, zk::k_batch_normalize, blocks_for((total + nbatch - 1) / nbatch),
+           (const G1J*)J, total, nbatch, dptr<G1A>(k->basis));
     sync(c);
     *out = k.release();
   });

@@ -19,11 +19,7 @@
 namespace zk {
 
 constexpr uint32_t kSegTask = 32;    // points summed by one thread per reduction level
-#ifndef ZK_BUCKET_CHUNK
-#define ZK_BUCKET_CHUNK 32
-#endif
-constexpr uint32_t kBucketChunk = ZK_BUCKET_CHUNK;  // buckets per thread in the window reduction (<= 32: c >= 6)
-static_assert(kBucketChunk <= 32, "the smallest window (c = 6) has 32 buckets");
+constexpr uint32_t kBucketChunkMax = 32;  // buckets per thread in the window reduction (host-chosen, a power of two <= 32: c >= 6)
 
 __device__ __forceinline__ Fq ld_fq(const Fq* p, uint64_t i) { return p[i]; }
 
@@ -245,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
 
 // ---- balanced bucket sums (round 5) ---------------------------------------------------
 // The sorted entries (point order, bucket slot order) cut into equal tasks of
-// kBalTask consecutive entries, one per thread, regardless of bucket
+// `task` consecutive entries, one per thread, regardless of bucket
 // boundaries — k_seg_sum<true> gave each bucket its own tasks of <= 32, so a
 // wave ran 32 iterations for tasks averaging ~22 (random scalars: ~32 entries
 // per bucket), ~70 % of its lanes busy. A thread emits one XYZZ partial per
@@ -254,17 +250,17 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum(const G1A* __restrict__ base
 // infinity of every empty slot; k_seg_sum_xyzz then sums each slot's partials
 // (usually 1 or 2) to its Jacobian bucket sum. Group arithmetic is exact, so
 // the bucket sums are the same group elements as before.
-#ifndef ZK_BAL_TASK
-#define ZK_BAL_TASK 64
-#endif
-constexpr uint32_t kBalTask = ZK_BAL_TASK;
+// (task = entries per thread, host-chosen: kBalTaskMax for large MSMs, fewer
+// when that would leave the GPU with too few threads — a small MSM's time is
+// one thread's serial chain of additions)
+constexpr uint32_t kBalTaskMax = 64;
 // partials of slot s: one per task its entries touch (an empty slot: 1, its infinity)
-__global__ __launch_bounds__(kBlock) void k_bal_counts(const uint32_t* __restrict__ cnt, uint64_t nseg,
+__global__ __launch_bounds__(kBlock) void k_bal_counts(const uint32_t* __restrict__ cnt, uint64_t nseg, uint32_t task,
                                                        uint32_t* __restrict__ counts) {
   const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (s >= nseg) return;
   const uint32_t a = cnt[s], b = cnt[s + 1];
-  counts[s] = a == b ? 1u : (b - 1) / kBalTask - a / kBalTask + 1;
+  counts[s] = a == b ? 1u : (b - 1) / task - a / task + 1;
 }
 __global__ __launch_bounds__(kBlock) void k_bal_empty(const uint32_t* __restrict__ cnt, uint64_t nseg,
                                                       const uint32_t* __restrict__ pbal, G1XYZZ* __restrict__ out) {
@@ -275,12 +271,12 @@ __global__ __launch_bounds__(kBlock) void k_bal_empty(const uint32_t* __restrict
 __global__ __launch_bounds__(kBlock) void k_seg_sum_bal(const G1A* __restrict__ bases, uint64_t nbases,
                                                         const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ cnt, uint64_t nseg, uint32_t total,
-                                                        const uint32_t* __restrict__ pbal, uint64_t npart,
-                                                        G1XYZZ* __restrict__ out) {
+                                                        uint32_t tsize, const uint32_t* __restrict__ pbal,
+                                                        uint64_t npart, G1XYZZ* __restrict__ out) {
   const uint64_t task = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t lo = task * kBalTask;
+  const uint64_t lo = task * tsize;
   if (lo >= total) return;
-  const uint32_t hi = (uint32_t)(lo + kBalTask < total ? lo + kBalTask : total);
+  const uint32_t hi = (uint32_t)(lo + tsize < total ? lo + tsize : total);
   // the slot holding entry lo: the first s with cnt[s + 1] > lo
   uint64_t L = 0, H = nseg - 1;
   while (L < H) {
@@ -291,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum_bal(const G1A* __restrict__ 
   uint64_t s = L;
   uint32_t a = cnt[s], b = cnt[s + 1];
   auto emit = [&](const G1XYZZ& acc) {
-    const uint64_t at = pbal[s] + (task - a / kBalTask);
+    const uint64_t at = pbal[s] + (task - a / tsize);
     ZK_DCHECK(at < npart && at < pbal[s + 1]);
     out[at] = acc;
   };
@@ -337,8 +333,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_sum_xyzz(const G1XYZZ* __restric
 // out[w (chunks + 1) + j]; W more threads put 2^c B_0 (bucket 0 holds the
 // digits of magnitude 2^c, signed_digits) at out[w (chunks + 1) + chunks].
 __global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict__ buckets, uint32_t c, uint32_t W,
-                                                          G1J* __restrict__ out) {
-  const uint32_t chunks = (1u << c) / kBucketChunk;
+                                                          uint32_t bchunk, G1J* __restrict__ out) {
+  const uint32_t chunks = (1u << c) / bchunk;
   const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
   if (g >= W * (chunks + 1)) return;
   if (g >= W * chunks) {
@@ -348,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict_
     out[w * (chunks + 1) + chunks] = z;
     return;
   }
-  const uint32_t w = g / chunks, j = g % chunks, lo = j * kBucketChunk, hi = lo + kBucketChunk;
+  const uint32_t w = g / chunks, j = g % chunks, lo = j * bchunk, hi = lo + bchunk;
   const G1J* B = buckets + ((uint64_t)w << c);
   G1J t = g1_inf(), u = g1_inf();
   for (uint32_t d = hi; d-- > lo;) {
@@ -440,16 +436,16 @@ __global__ __launch_bounds__(kBlock) void k_eq_scalars(const Fe* __restrict__ ta
   }
 }
 
-// Jacobian -> affine, kBatchNorm points per thread sharing one inversion
+// Jacobian -> affine, `batch` (<= kBatchNorm) points per thread sharing one inversion
 // (Montgomery's trick); the prefix products are parked in out[].x until the
 // backward pass overwrites them; infinity stays (0, 0)
-constexpr uint32_t kBatchNorm = 64;
-__global__ __launch_bounds__(kBlock) void k_batch_normalize(const G1J* __restrict__ in, uint64_t n,
+constexpr uint32_t kBatchNorm = 64;  // (host: fewer for small sets, the inversion is a serial chain)
+__global__ __launch_bounds__(kBlock) void k_batch_normalize(const G1J* __restrict__ in, uint64_t n, uint32_t batch,
                                                             G1A* __restrict__ out) {
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t a = t * kBatchNorm;
+  const uint64_t a = t * batch;
   if (a >= n) return;
-  const uint32_t m = (uint32_t)(n - a < kBatchNorm ? n - a : kBatchNorm);
+  const uint32_t m = (uint32_t)(n - a < batch ? n - a : batch);
   Fq acc = fq_one();
   for (uint32_t k = 0; k < m; ++k) {
     out[a + k].x = acc;  // product of the nonzero Z's before k
