@@ -70,7 +70,7 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
   const uint32_t* cur_off = off;
   int flip = 0;
   for (int level = 0;; ++level) {
-    require(level < 12, "segmented reduction did not converge");
+    require(level < 64, "segmented reduction did not converge");  // (task >= 2: <= 32 levels for 2^32 items)
     DevBuf& toff = c->msm[pool + flip];
     DevBuf& tseg = c->msm[pool + 2];
     DevBuf& part = c->msm[pool + 3 + flip];
