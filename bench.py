@@ -855,12 +855,18 @@ def main() -> None:
     muls = sum(v["field_muls"] for v in k.values()) / args.steps
 
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "r4_traffic.json")
+    import glob
+    import re
+
+    # the newest round's PMC traffic file (profiles/r<N>_traffic.json, tools/pmc_traffic.py)
+    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")),
+                    key=lambda f: int(re.match(r"r(\d+)_", os.path.basename(f)).group(1)))
+    tpath = tfiles[-1] if tfiles else ""
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
         if t.get("kind") == dom and field == 0:  # the longest launch of this workload
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
-            traffic_src = f"profiles/r4_traffic.json ({t['method']}); traffic/alg = {t['traffic_over_alg']:.4f}"
+            traffic_src = f"profiles/{os.path.basename(tpath)} ({t['method']}); traffic/alg = {t['traffic_over_alg']:.4f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
     comm = ctx.comm_info()  # what the attached communicator reports (RCCL: ncclCommCount / ncclCommUserRank)
     if comm["kind"] != "none" and (comm["count"] != world or comm["rank"] != rank):
