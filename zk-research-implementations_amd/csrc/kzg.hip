@@ -190,13 +190,24 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   chb.ensure((size_t)W * (chunks + 1) * sizeof(G1J));
   launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * (chunks + 1)), (const G1J*)buckets, bb, W, bchunk,
          dptr<G1J>(chb));
-  std::vector<uint32_t> woff(W + 1);
-  for (uint32_t w = 0; w <= W; ++w) woff[w] = w * (chunks + 1);
-  DevBuf& wo = c->msm[14];
-  wo.ensure((W + 1) * 4);
-  HIPCK(hipMemcpyAsync(wo.p, woff.data(), (W + 1) * 4, hipMemcpyHostToDevice, c->stream));
-  // (few, long segments: short tasks keep the levels parallel instead of 32 serial additions per thread)
-  G1J* ws = seg_reduce(c, nullptr, 0, nullptr, dptr<G1J>(chb), dptr<uint32_t>(wo), W, 5, nullptr, c->msm_win_task);
+  // the W window sums: equal segments of chunks + 1 points, reduced in levels
+  // of msm_win_task points per thread (short tasks keep every level parallel;
+  // the sizes are known here, so no scans and no host syncs)
+  const G1J* ws = dptr<G1J>(chb);
+  {
+    uint32_t len = chunks + 1;
+    const uint32_t task = std::max<uint32_t>(2, c->msm_win_task);
+    int flip = 0;
+    while (len > 1) {
+      const uint32_t olen = (len + task - 1) / task;
+      DevBuf& ob = c->msm[5 + flip];
+      ob.ensure((size_t)W * olen * sizeof(G1J));
+      launch(c, ZK_K_MSM, 0, 0, k_sum_uniform, blocks_for((uint64_t)W * olen), ws, len, W, task, dptr<G1J>(ob));
+      ws = dptr<G1J>(ob);
+      len = olen;
+      flip ^= 1;
+    }
+  }
   std::vector<G1J> S(W);
   HIPCK(hipMemcpyAsync(S.data(), ws, W * sizeof(G1J), hipMemcpyDeviceToHost, c->stream));
   sync(c);

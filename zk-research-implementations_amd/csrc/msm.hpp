@@ -355,6 +355,23 @@ __global__ __launch_bounds__(kBlock) void k_window_chunks(const G1J* __restrict_
   out[w * (chunks + 1) + j] = lo ? g1_add(u, g1_mul_small(t, lo)) : u;  // d = 0 (lo = 0) has weight 0 here
 }
 
+// the window sums: nseg segments of exactly len consecutive Jacobian points,
+// `task` points per thread per level; out[s olen + k] = the sum of points
+// [k task, min((k + 1) task, len)) of segment s, olen = ceil(len / task).
+// The sizes are known on the host, so the levels need no scan and no sync.
+__global__ __launch_bounds__(kBlock) void k_sum_uniform(const G1J* __restrict__ in, uint32_t len, uint32_t nseg,
+                                                        uint32_t task, G1J* __restrict__ out) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t olen = (len + task - 1) / task;
+  if (t >= (uint64_t)nseg * olen) return;
+  const uint32_t s = (uint32_t)(t / olen), k = (uint32_t)(t % olen);
+  const uint64_t a = (uint64_t)s * len + (uint64_t)k * task;
+  const uint64_t e = (uint64_t)s * len + ((k + 1) * task < len ? (k + 1) * task : len);
+  G1J acc = g1_inf();
+  for (uint64_t j = a; j < e; ++j) acc = g1_add(acc, in[j]);
+  out[t] = acc;
+}
+
 // ---- fixed-base scalar multiplication (Lagrange basis setup) ----------------------
 // 16-bit windows: table16[w * 65536 + d] = d * 2^(16w) * G (affine), built on
 // the device from the 8-bit table (one mixed addition per entry, then one
