@@ -99,6 +99,27 @@ def test_grid_capped_steps_match_oracle(monkeypatch, n, cap):
         c.close()
 
 
+@pytest.mark.parametrize("pipe", ["0", "1"])
+@pytest.mark.parametrize("cap", ["1", "5", "0"])
+def test_t33_pipelined_and_plain_loops_match_oracle(monkeypatch, pipe, cap):
+    """The 64-octant k_gkr_t33 has two chunk loops (ZK_T33_PIPE=1, the default:
+    double-buffered image, the previous chunk's products interleaved with the
+    current chunk's folds and drained after the loop; 0: two barriers per
+    chunk). Both against the oracle with one chunk per block (cap 0 = no cap)
+    and with several (caps 1 and 5), where the drain and buffer swap matter."""
+    n = 21
+    want = oracle_proof(0, n, 23)
+    monkeypatch.setenv("ZK_T33_PIPE", pipe)
+    monkeypatch.setenv("ZK_T33_OCT64_MIN", "1")  # the 64-octant path at every t33 step that has a chunk per CU
+    if cap != "0":
+        monkeypatch.setenv("ZK_GRID_CAP", cap)
+    c = zk_amd.Context(0)
+    try:
+        assert device_proof(c, 0, n, 23) == want
+    finally:
+        c.close()
+
+
 def test_grid_capped_headline_matches_fixture(monkeypatch):
     g = LARGE["bn254_fr_24_s3"]
     monkeypatch.setenv("ZK_GRID_CAP", "37")  # every step several chunks per block, odd grids

@@ -223,6 +223,7 @@ struct zk_ctx {
   uint32_t dtail_blocks = 64;           // at most this many blocks (<= 64: atomic fan-in) (ZK_DTAIL_BLOCKS)
   uint32_t gather_vars = 10;  // sharded: gather the tables once <= this many local rounds remain, finish locally (ZK_GATHER_VARS; 0: at the end)
   DevBuf gbuf;                // sharded gather: fold scratch, the one-hot buffer, the interleaved global tables
+  bool t33_pipe = true;  // ZK_T33_PIPE (0: off): the 64-octant k_gkr_t33 with a double-buffered image, products interleaved
   uint32_t t33_oct64_min = 4;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
@@ -933,8 +934,12 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
           const uint64_t nch = O / 64;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64>);
           const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
-          launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64>, grid, cur[0], cur[1], cur[2], cur[3],
-                 nx[0], nx[1], nx[2], nx[3], O, din, sk);
+          if (c->t33_pipe)
+            launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64, true>, grid, cur[0], cur[1], cur[2],
+                   cur[3], nx[0], nx[1], nx[2], nx[3], O, din, sk);
+          else
+            launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64>, grid, cur[0], cur[1], cur[2], cur[3],
+                   nx[0], nx[1], nx[2], nx[3], O, din, sk);
         } else {
           const uint64_t nch = O / 32;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 32>);

@@ -27,6 +27,7 @@
 // layout (A[row = digit][k = point], B[k = point][col = digit]); operand
 // maps and the transposed read measured on the box (tools/microbench_mfma.hip).
 #pragma once
+#include <type_traits>
 #include "kernels.hpp"
 
 namespace zk {
@@ -901,7 +902,22 @@ struct T33Scratch {
   Fe eqw[8];
 };
 
-template <class F, int OCT>
+// PIPE (OCT 64, ZK_T33_PIPE): a double-buffered image and ONE barrier per
+// chunk; the previous chunk's 64 product MFMAs run in four groups of 16 after
+// folds 1, 3, 5 and 7 of the current chunk (while its loads are in flight)
+// instead of after a second barrier
+struct T33ScratchP {
+  uint8_t img[2][8][4][64][32];  // [buffer][corner][table][octant][digit row]
+  unsigned long long T[kD0TCats][64];
+  uint64_t w17[kD0TCats][17];
+  uint64_t tot[kSlotU64];
+  uint64_t pp[kBlock];
+  uint32_t am_last;
+  uint32_t p2w[9][8];
+  Fe eqw[8];
+};
+
+template <class F, int OCT, bool PIPE = false>
 __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
@@ -956,7 +972,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
     }
   };
   if (early) first_loads();
-  __shared__ T33Scratch sc;
+  static_assert(!PIPE || OCT == 64, "the pipelined loop is the 64-octant one");
+  using Scratch = std::conditional_t<PIPE, T33ScratchP, T33Scratch>;
+  __shared__ Scratch sc;
   block_get_eq8<F>(din, sc.eqw, gridDim.x > 1);  // eq(r, c), the oldest pending challenge on c's top bit
   if (!early && (uint64_t)blockIdx.x < nch) first_loads();
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 1);
@@ -975,7 +993,62 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   for (int i = 0; i < 9; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[i][r] = 0;
-  if constexpr (OCT == 64) {
+  if constexpr (OCT == 64 && PIPE) {
+  uint8_t(*img2)[8][4][64][32] = reinterpret_cast<uint8_t(*)[8][4][64][32]>(&sc.img[0][0][0][0][0]);
+  const uint32_t aX = w >> 1, aY = w & 1;
+  auto products = [&](uint32_t b, int grp) {  // group grp = (pp, K half) of a chunk's products from image b
+    const int pp = grp >> 1, half = grp & 1;
+    i32x4 fa[4], fb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      fa[k] = tr_frag(&img2[b][4 * aX + k][2 * pp][32 * half][0]);
+      fb[k] = tr_frag(&img2[b][4 * aY + k][2 * pp + 1][32 * half][0]);
+    }
+#pragma unroll
+    for (int ux = 0; ux < 4; ++ux)
+#pragma unroll
+      for (int vy = 0; vy < 4; ++vy) {
+        const int slot = 3 * moment_digit(ux >> 1, vy >> 1) + moment_digit(ux & 1, vy & 1);
+        acc[slot] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[ux], fb[vy], acc[slot], 0, 0, 0);
+      }
+  };
+  uint32_t buf = 0;
+  bool prev = false;
+  for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x, buf ^= 1) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      i32x16 a0, a1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0;
+      {
+        Fe x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          x[k] = nx[k];
+          nx[k] = nx2[k];
+        }
+        const int u2 = f + 2;  // the fold two ahead
+        if (u2 < 8)
+          unit_at(ch, u2, nx2);
+        else
+          unit_at(ch + gridDim.x, u2 - 8, nx2);
+        fold_acc8(x, wf, a0, a1);
+      }
+      int64_t W[8];
+      fold_words(a0, a1, W);
+      const Fe z = dm_finish<F>(W, fe_zero<F>());
+      ZK_DCHECK(ch * 64 + l + (uint64_t)f * O < 8 * O);
+      st_fold(X2, ch * 64 + l + (uint64_t)f * O, z);
+      dm_row<F>(img2[buf][f][w][l], z);
+      if ((f & 1) && prev) products(buf ^ 1, f >> 1);  // the previous chunk's products, a quarter at a time
+    }
+    __syncthreads();  // this chunk's image is complete; the previous one's products are done (its buffer is free)
+    prev = true;
+  }
+  if (prev)
+#pragma unroll
+    for (int grp = 0; grp < 4; ++grp) products(buf ^ 1, grp);  // the last chunk's products
+  } else if constexpr (OCT == 64) {
   uint8_t(*img)[4][64][32] = reinterpret_cast<uint8_t(*)[4][64][32]>(&sc.img[0][0][0][0][0]);
   for (uint64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {
 #pragma unroll

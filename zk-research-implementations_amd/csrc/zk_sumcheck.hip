@@ -59,6 +59,7 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_ATOMIC_FANIN")) c->atomic_fanin = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_DTAIL_BLOCKS")) c->dtail_blocks = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_GATHER_VARS")) c->gather_vars = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char* e = getenv("ZK_T33_PIPE")) c->t33_pipe = atoi(e) != 0;
     if (const char* e = getenv("ZK_MSM_BALANCED")) c->msm_balanced = atoi(e) != 0;
     if (const char* e = getenv("ZK_MSM_WIN_TASK")) c->msm_win_task = std::max<uint32_t>(2u, (uint32_t)strtoul(e, nullptr, 0));
     if (const char* e = getenv("ZK_T33_OCT64_MIN")) c->t33_oct64_min = (uint32_t)strtoul(e, nullptr, 0);
