@@ -53,6 +53,11 @@ def parse():
                     "on one card, a gloo host all-reduce with every rank on device LOCAL_RANK %% device_count")
     ap.add_argument("--force-rccl", action="store_true",
                     help="diagnostic: at world 1 route every step through ncclAllReduce (the multi-rank data path)")
+    ap.add_argument("--reduce", default="rccl", choices=["rccl", "peer"],
+                    help="N>1 (or --force-rccl): each step's sums through an all-reduce on the communicator (default) "
+                    "or through the ranks' IPC-mapped peer buffers, summed by the step kernels (zk_ctx_attach_peer_reduce)")
+    ap.add_argument("--no-peer-leg", action="store_true",
+                    help="N>1 over RCCL: skip the side leg that reruns the headline with --reduce peer in fresh ranks")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
     ap.add_argument("--no-plain", action="store_true",
                     help="skip BASELINE config 1 (12-var plain prove, CPU port) and the GPU plain prove/verify legs")
@@ -617,7 +622,7 @@ def _free_port() -> int:
 
 
 def spawn_ranks(n: int, cmd: list, env_extra: dict | None = None, grace_s: float = 10.0,
-                poll_s: float = 0.2) -> tuple[int, str]:
+                poll_s: float = 0.2, timeout_s: float | None = None) -> tuple[int, str]:
     """Launcher for `bench.py --gpus N` run without torch.distributed.run: start
     `cmd` as N fresh child processes, one per GPU, with RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what torchrun would set), and
@@ -627,7 +632,8 @@ def spawn_ranks(n: int, cmd: list, env_extra: dict | None = None, grace_s: float
     When a rank exits non-zero the others are given `grace_s` to finish, then
     killed (their peers would otherwise wait at a barrier). Returns (exit code,
     rank 0's stdout): 0 only if every rank exited 0, else the first failing
-    rank's code (a signal death maps to 128 + signal)."""
+    rank's code (a signal death maps to 128 + signal). With `timeout_s`, ranks
+    still running after it are killed and the result is a failure (124)."""
     import signal
 
     env0 = dict(os.environ)
@@ -646,8 +652,14 @@ def spawn_ranks(n: int, cmd: list, env_extra: dict | None = None, grace_s: float
     reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
     reader.start()
     first_bad, t_bad = None, None
+    t_start = time.monotonic()
     while True:
         codes = [p.poll() for p in procs]
+        if timeout_s is not None and first_bad is None and time.monotonic() - t_start > timeout_s \
+                and any(c is None for c in codes):
+            print(f"bench launcher: ranks still running after {timeout_s:.0f} s", file=sys.stderr)
+            first_bad, t_bad = -1, time.monotonic() - grace_s - 1  # kill now
+            continue
         if first_bad is None:
             for r, c in enumerate(codes):
                 if c is not None and c != 0:
@@ -673,6 +685,8 @@ def spawn_ranks(n: int, cmd: list, env_extra: dict | None = None, grace_s: float
     if first_bad is None:
         bad = [c for c in codes if c != 0]
         rc = bad[0] if bad else 0
+    elif first_bad < 0:
+        rc = 124
     else:
         rc = codes[first_bad]
     if rc < 0:
@@ -729,6 +743,8 @@ def main() -> None:
     ctx = zk_amd.Context(local)
     if args.force_rccl and world == 1:
         ctx.attach_rccl(0, 1, rccl_unique_id())
+        if args.reduce == "peer":
+            ctx.attach_peer_reduce()
     lg = (world - 1).bit_length()
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -744,6 +760,8 @@ def main() -> None:
             obj = [rccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             ctx.attach_rccl(rank, world, obj[0])
+        if args.reduce == "peer":
+            ctx.attach_peer_reduce()  # collective; checked across the world, raises if it fails
 
     nloc = args.nvars
     n = nloc + lg
@@ -868,6 +886,32 @@ def main() -> None:
             traffic = t["traffic_bytes_per_launch"]  # HBM bytes per launch, beside alg_bytes_per_launch
             traffic_src = f"profiles/{os.path.basename(tpath)} ({t['method']}); traffic/alg = {t['traffic_over_alg']:.4f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
+    peer_leg = None
+    if world > 1 and args.comm == "rccl" and args.reduce == "rccl" and not args.no_peer_leg:
+        # the headline again with --reduce peer, in N fresh ranks that rank 0
+        # starts as child processes (one per GPU): a failure or hang there can
+        # only cost the side field, never this line
+        if rank == 0:
+            cmd = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(world), "--steps", str(args.steps),
+                   "--warmup", str(args.warmup), "--nvars", str(args.nvars), "--field", args.field, "--seed",
+                   str(args.seed), "--reduce", "peer", "--no-config4", "--no-peer-leg"]
+            t_leg = time.perf_counter()
+            rc, text = spawn_ranks(world, cmd, timeout_s=300.0)
+            lines = [ln for ln in text.splitlines() if ln.strip()]
+            peer_leg = {"cmd": " ".join(cmd[2:]), "rc": rc, "wall_s": round(time.perf_counter() - t_leg, 1)}
+            if rc == 0 and lines:
+                try:
+                    r = json.loads(lines[-1])
+                    peer_leg.update({"value": r["value"], "ms_per_step": r["ms_per_step"], "proof": r["proof"],
+                                     "reduce": r.get("reduce"), "comm": r.get("comm"),
+                                     "collectives_per_step": r["breakdown_per_step"]["collectives"],
+                                     "launches_of_proof": r["roofline"]["launches_of_proof"],
+                                     "vs_rccl": r["value"] / value})
+                except (ValueError, KeyError) as e:
+                    peer_leg["error"] = f"unreadable result line: {e}"
+            else:
+                peer_leg["error"] = "the peer-reduction ranks failed (their stderr is in this run's log)"
+        barrier()
     comm = ctx.comm_info()  # what the attached communicator reports (RCCL: ncclCommCount / ncclCommUserRank)
     if comm["kind"] != "none" and (comm["count"] != world or comm["rank"] != rank):
         raise SystemExit(f"communicator reports rank {comm['rank']} of {comm['count']}, expected {rank} of {world}")
@@ -892,11 +936,15 @@ def main() -> None:
                 "nvars_total": n,
                 "nvars_per_gpu": nloc,
                 "parallelism": f"hypercube split over {world} GPU(s) by low index bits; "
-                + ("1 RCCL all-reduce of the step's limb sums (<= 243 x u64) per step of 2-3 rounds" if args.comm == "rccl" else
+                + ("the step kernels sum the step's limb sums (<= 243 x u64) across ranks through IPC-mapped peer "
+                   "buffers, one exchange per step of 2-3 rounds" if ctx.peer_reduce else
+                   "1 RCCL all-reduce of the step's limb sums (<= 243 x u64) per step of 2-3 rounds" if args.comm == "rccl" else
                    "host (gloo) all-reduce per round: diagnostic, not the product path") if world > 1 else "single GPU",
             },
             "proof": digest,
             "comm": comm,
+            "reduce": ("peer" if ctx.peer_reduce else "rccl" if comm["kind"] == "rccl" else comm["kind"])
+            if comm["kind"] != "none" else None,
             "rccl_ranks": comm["count"] if comm["kind"] == "rccl" else None,
             "launcher": os.environ.get("ZK_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
             "roofline": {
@@ -945,6 +993,8 @@ def main() -> None:
             }
         if cfg4 is not None:
             out["config4_26var"] = cfg4
+        if peer_leg is not None:
+            out["peer_reduce_leg"] = peer_leg
         if not args.no_e2e and world == 1:
             e2e = e2e_bench(ctx, field, tabs, n)
             e2e["same_proof_as_device_resident"] = bool(np.array_equal(e2e.pop("challenges"), ch))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 13u
+#define ZK_ABI_VERSION 14u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -385,6 +385,19 @@ int zk_ctx_detach_comm(zk_ctx* ctx);
  * communicator reports them (ncclCommUserRank / ncclCommCount), else the
  * attached rank / world (0 / 1 with none). */
 int zk_ctx_comm_count(const zk_ctx* ctx, int* out_kind, int* out_rank, int* out_count);
+/* Peer reduction (collective: every rank calls it, after attaching a
+ * communicator; world <= 8, the ranks of one node). enable = 1: each rank
+ * allocates an uncached receive buffer, the IPC handles are exchanged through
+ * the attached communicator and opened, and one reduction of known values is
+ * checked across the world. From then on each sharded step's sums are
+ * summed by the step kernel itself — its publishing block writes them into
+ * every rank's buffer and waits for the others' (replacing the step's
+ * all-reduce of sum_check_protocol.rs:96-108's round sums; the gather stays on
+ * the communicator). enable = 0 releases it. Proofs must then run in the same
+ * order on every rank (the reductions carry a shared sequence number); a proof
+ * that fails mid-way leaves the sequence unusable until the next attach.
+ * *out_ok (may be null) = 1 when enabled and the check passed. */
+int zk_ctx_attach_peer_reduce(zk_ctx* ctx, int enable, int* out_ok);
 /* gkr_prove over the global (nvars_local + log2(world))-variable SumPoly whose
  * local shard this rank holds; outputs are the global proof (identical on all
  * ranks). out arrays sized for nvars_local + log2(world) rounds. */

@@ -2,7 +2,8 @@
 tests/test_gpu_sharded.py; not a test module itself).
 
 env: RANK, WORLD_SIZE, MASTER_PORT, COMM in {host, rccl, none}, FIELD, NLOCAL, OUT
-(+ optional SEED, default 19)
+(+ optional SEED, default 19; PEER=1: zk_ctx_attach_peer_reduce after the
+communicator, so the steps' sums meet in the ranks' IPC-mapped buffers)
 Rank g proves its low-index-bit shard; rank 0 writes the proof as JSON.
 """
 from __future__ import annotations
@@ -34,6 +35,9 @@ def main() -> None:
         ctx.attach_host_comm(rank, world, TorchAllreduce())
     elif comm == "rccl":
         rendezvous_rccl(ctx, rank, world)
+    if os.environ.get("PEER") == "1":
+        ctx.attach_peer_reduce()
+        ctx.reset_stats()  # (the handle exchange went through the communicator)
     i0, stride = shard_layout(rank, world)
     seed = int(os.environ.get("SEED", "19"))
     tabs = [ctx.synth(field, 1 << nloc, seed=seed, table=t, index0=i0, stride=stride) for t in range(4)]
@@ -55,7 +59,7 @@ def main() -> None:
     res = {"polys": [[hex(x) for x in p] for p in polys],
            "chal": [hex(x) for x in to_ints(ch[:n])], "collectives": ctx.stats()["collectives"],
            "blob_keccak": zk_amd.keccak256(blob).hex(), "blob_keccak_claimed": zk_amd.keccak256(blob_c).hex(),
-           "comm": ctx.comm_info()}
+           "comm": ctx.comm_info(), "peer": ctx.peer_reduce}
     with open(os.path.join(os.environ["OUT"], f"rank{rank}.json"), "w") as fh:
         json.dump(res, fh)
     dist.barrier()

@@ -79,3 +79,21 @@ def test_world_mismatch_is_refused():
                        timeout=120)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_timeout_kills_hung_ranks():
+    """The N>1 bench's peer-reduction side leg starts its ranks with a time
+    limit: ranks still running after it are killed and the leg reads as failed
+    (124), so a hang there cannot hold the headline line."""
+    code = "import time; time.sleep(600)"
+    t0 = time.monotonic()
+    rc, text = bench.spawn_ranks(2, [sys.executable, "-c", code], grace_s=1.0, timeout_s=2.0)
+    assert rc == 124
+    assert time.monotonic() - t0 < 60
+    assert text == ""
+
+
+def test_timeout_does_not_touch_ranks_that_finish():
+    code = "import os; print('{\"ok\": 1}') if os.environ['RANK'] == '0' else None"
+    rc, text = bench.spawn_ranks(2, [sys.executable, "-c", code], timeout_s=120.0)
+    assert rc == 0 and json.loads(text.splitlines()[-1]) == {"ok": 1}

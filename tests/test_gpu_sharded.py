@@ -160,3 +160,45 @@ def test_config4_workload_8_ranks_matches_fixture(tmp_path):
         assert r["blob_keccak_claimed"] == fix["blob_keccak256"], f"rank {rank}"
         assert r["collectives"] == _collectives(23), f"rank {rank}"
         assert r["comm"] == {"kind": "host", "rank": rank, "count": 8}
+
+
+# Peer reduction (zk_ctx_attach_peer_reduce): each step's publishing block
+# writes its sums into every rank's IPC-mapped receive buffer and sums the
+# world's itself. On this one card the ranks are processes sharing the device
+# (host communicator for the handle exchange and the gather; steps launch after
+# their challenges); at world 1 over RCCL (ZK_FORCE_COLLECTIVES=1) it runs the
+# product schedule: pre-enqueued steps, no RCCL all-reduce or publish kernel.
+@pytest.mark.parametrize("world,nloc,field,gather", [(2, 12, 0, "10"), (2, 16, 2, "0"), (4, 13, 1, "6"), (8, 14, 0, "10"),
+                                                     (8, 10, 2, "0"), (2, 20, 0, "10"), (4, 0, 0, "10")])
+def test_peer_reduce_ranks_match_single_process(tmp_path, world, nloc, field, gather):
+    res = _run(world, "host", field, nloc, str(tmp_path), {"PEER": "1", "ZK_GATHER_VARS": gather})
+    want = _oracle(field, nloc + world.bit_length() - 1)
+    for rank, r in enumerate(res):
+        assert r["peer"] is True, f"rank {rank}"
+        assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
+
+
+@pytest.mark.parametrize("nloc,gather", [(14, "0"), (14, "10"), (20, "10"), (24, "10")])
+def test_peer_reduce_forced_at_world1_rccl(tmp_path, nloc, gather):
+    res = _run(1, "rccl", 0, nloc, str(tmp_path), {"PEER": "1", "ZK_FORCE_COLLECTIVES": "1", "ZK_GATHER_VARS": gather,
+                                                    "SEED": "3" if nloc == 24 else "19"})
+    assert res[0]["peer"] is True
+    if nloc == 24:  # the headline workload: the committed fixture
+        fix = json.load(open(os.path.join(ROOT, "tests", "golden", "large.json")))["bn254_fr_24_s3"]
+        assert res[0]["chal"] == [hex(int(c, 16)) for c in fix["challenges"]]
+        assert res[0]["blob_keccak_claimed"] == fix["blob_keccak256"]
+        return
+    want = _oracle(0, nloc)
+    assert {"polys": res[0]["polys"], "chal": res[0]["chal"], "blob_keccak": res[0]["blob_keccak"]} == want
+    assert res[0]["collectives"] == _collectives(nloc, int(gather))
+
+
+def test_peer_reduce_config4_workload_8_ranks(tmp_path):
+    """Config 4 (26 variables over 8 ranks) with the steps' sums through the
+    peer buffers: every rank's proof equals the committed fixture."""
+    fix = json.load(open(os.path.join(ROOT, "tests", "golden", "large.json")))["bn254_fr_26_s4"]
+    res = _run(8, "host", 0, 23, str(tmp_path), {"SEED": "4", "PEER": "1"})
+    for rank, r in enumerate(res):
+        assert r["peer"] is True
+        assert r["chal"] == [hex(int(c, 16)) for c in fix["challenges"]], f"rank {rank}"
+        assert r["blob_keccak_claimed"] == fix["blob_keccak256"], f"rank {rank}"

@@ -242,6 +242,13 @@ struct zk_ctx {
   uint32_t rtag = 0;        // last tag handed to a pre-enqueued round kernel
   void* user = nullptr;
   ncclComm_t nccl = nullptr;
+  // peer reduction (zk_ctx_attach_peer_reduce): the sharded steps' sums meet
+  // in the ranks' IPC-mapped receive buffers instead of an RCCL all-reduce
+  bool peer = false;
+  uint64_t* peer_buf = nullptr;       // our receive buffer (uncached device memory)
+  std::vector<void*> peer_open;       // the peers' buffers, opened from their IPC handles
+  zk::PeerSlots* d_peer = nullptr;    // device copy of the slot table
+  uint64_t peer_seq = 0;              // last reduction's sequence tag (the same on every rank)
   // KZG / MSM scratch (grow-only) and the cached fixed-base table of G1
   DevBuf msm[19];
   bool msm_balanced = true;  // ZK_MSM_BALANCED: bucket sums in equal tasks across bucket boundaries (kzg.hip)
@@ -443,6 +450,86 @@ inline void allreduce_host(zk_ctx* c, uint64_t* w, size_t n) {
   c->stats.collectives += 1;
 }
 
+// Peer reduction set-up / tear-down (zk_ctx_attach_peer_reduce).
+inline void peer_release(zk_ctx* c) {
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void* p : c->peer_open) (void)hipIpcCloseMemHandle(p);
+  c->peer_open.clear();
+  if (c->d_peer) (void)hipFree(c->d_peer);
+  if (c->peer_buf) (void)hipFree(c->peer_buf);
+  c->d_peer = nullptr;
+  c->peer_buf = nullptr;
+  c->peer = false;
+  c->peer_seq = 0;
+}
+
+// One reduction of known values (rank g contributes (g + 1)(t + 1) in word t)
+// through the same device path as the steps; the host checks the world's sum.
+static __global__ void k_peer_check(zk::RoundSink sk) {
+  __shared__ zk::LimbScratch<16> sc;
+  const uint32_t t = threadIdx.x;
+  if (t < 16) sc.tot[t] = (uint64_t)(sk.peer->rank + 1) * (t + 1);
+  __syncthreads();
+  zk::publish_limbs<16>(sc, sk);
+}
+
+inline void peer_attach(zk_ctx* c) {
+  const size_t bytes = 2 * (size_t)c->world * zk::kPeerSlotU64 * sizeof(uint64_t);
+  HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_buf), bytes, hipDeviceMallocUncached));
+  HIPCK(hipMemset(c->peer_buf, 0, bytes));
+  HIPCK(hipDeviceSynchronize());
+  hipIpcMemHandle_t h;
+  HIPCK(hipIpcGetMemHandle(&h, c->peer_buf));
+  constexpr size_t HW = (sizeof(hipIpcMemHandle_t) + 7) / 8;
+  std::vector<uint64_t> w(HW * c->world, 0);
+  memcpy(&w[HW * c->rank], &h, sizeof h);
+  allreduce_host(c, w.data(), w.size());  // disjoint slots: the sum is the gather
+  zk::PeerSlots ps{};
+  ps.world = (uint32_t)c->world;
+  ps.rank = (uint32_t)c->rank;
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) {
+      ps.slot[r] = c->peer_buf;
+      continue;
+    }
+    hipIpcMemHandle_t hr;
+    memcpy(&hr, &w[HW * r], sizeof hr);
+    void* p = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      peer_release(c);
+      fail(ZK_ECOMM, std::string("peer reduction: opening rank ") + std::to_string(r) + "'s buffer: " + hipGetErrorString(e));
+    }
+    c->peer_open.push_back(p);
+    ps.slot[r] = reinterpret_cast<uint64_t*>(p);
+  }
+  HIPCK(hipMalloc(reinterpret_cast<void**>(&c->d_peer), sizeof ps));
+  HIPCK(hipMemcpy(c->d_peer, &ps, sizeof ps, hipMemcpyHostToDevice));
+  c->peer = true;
+  c->peer_seq = 0;
+  // the check: the same publish path, a reduction every rank takes part in
+  zk::RoundSink sk{};
+  sk.host_out = c->h_red;
+  sk.host_flag = h_flag(c);
+  sk.tag = ++c->tag;
+  sk.peer = c->d_peer;
+  sk.peer_seq = ++c->peer_seq;
+  sk.err = h_err(c);
+  __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
+  k_peer_check<<<1, zk::kBlock, 0, c->stream>>>(sk);
+  HIPCK(hipGetLastError());
+  HIPCK(hipStreamSynchronize(c->stream));
+  const uint32_t err = __atomic_load_n(h_err(c), __ATOMIC_ACQUIRE);
+  bool ok = err == 0 && __atomic_load_n(h_flag(c), __ATOMIC_ACQUIRE) == sk.tag;
+  const uint64_t tri = (uint64_t)c->world * (c->world + 1) / 2;
+  for (uint64_t t = 0; t < 16 && ok; ++t) ok = __atomic_load_n(c->h_red + t, __ATOMIC_RELAXED) == tri * (t + 1);
+  if (!ok) {
+    __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
+    peer_release(c);
+    fail(ZK_ECOMM, err ? "peer reduction check: a peer never arrived" : "peer reduction check: wrong sums");
+  }
+}
+
 inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   zk::RoundSink s;
   s.trace = c->tail_trace ? c->tail_trace + 512 : nullptr;  // ZK_DEBUG_TAIL: per-step stamps
@@ -452,10 +539,15 @@ inline zk::RoundSink make_sink(zk_ctx* c, bool across_ranks) {
   s.counter = d_counter(c);
   s.accum = d_accum(c);
   s.tag = ++c->tag;
-  const bool via_rccl = across_ranks && multi_rank(c) && c->comm == COMM_RCCL;
+  const bool via_peer = across_ranks && multi_rank(c) && c->peer;
+  const bool via_rccl = across_ranks && multi_rank(c) && c->comm == COMM_RCCL && !via_peer;
   s.dev_out = via_rccl ? d_red(c) : nullptr;
   s.host_out = via_rccl ? nullptr : c->h_red;
   s.host_flag = via_rccl ? nullptr : h_flag(c);
+  s.peer = via_peer ? c->d_peer : nullptr;
+  s.peer_seq = via_peer ? ++c->peer_seq : 0;
+  s.err = h_err(c);
+  if (via_peer) c->stats.collectives += 1;
   return s;
 }
 
@@ -487,7 +579,7 @@ inline void wait_flag(zk_ctx* c, uint32_t tag) {
 // Stream side of a round's hand-off, enqueued right after its kernel: across
 // ranks over RCCL the device totals are all-reduced and then published.
 inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
-  if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL) {
+  if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL && !c->peer) {
     {
       CollTimer ct(c, 8.0 * n);
       NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
@@ -506,11 +598,12 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
   const bool multi = across_ranks && multi_rank(c);
   const int n = K * L;
   wait_flag(c, sk.tag);
-  if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) != 0)
-    fail(ZK_EDEVICE, "a pre-enqueued round kernel waited more than 1 s for its challenge");
+  if (const uint32_t e = __atomic_load_n(h_err(c), __ATOMIC_ACQUIRE))
+    fail(ZK_EDEVICE, e == 2u ? "a peer's sums never arrived (peer reduction, 10 s)"
+                             : "a pre-enqueued round kernel waited more than 1 s for its challenge");
   uint64_t w[K * 17 > 17 ? K * 17 : 17];
   for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
-  if (multi && c->comm == COMM_HOST) {
+  if (multi && c->comm == COMM_HOST && !c->peer) {
     CollTimer ct(c, 8.0 * n);
     if (c->ar(c->user, w, n) != 0) fail(ZK_ECOMM, "host all-reduce callback failed");
     c->stats.collectives += 1;
@@ -652,8 +745,9 @@ inline bool prelaunch(zk_ctx* c, uint32_t nv) {
 // Small rounds in one persistent kernel (k_gkr_tail, ZK_DROUND=0 only)?
 // Pre-enqueued only, and not when each round's sums take an RCCL all-reduce
 // on the stream (the kernel would hold the stream).
+// (Nor with peer reduction: its steps keep the RCCL schedule.)
 inline bool use_tail(zk_ctx* c, bool across_ranks) {
-  return c->tail && !(across_ranks && multi_rank(c) && c->comm == COMM_RCCL);
+  return c->tail && !(across_ranks && multi_rank(c) && (c->comm == COMM_RCCL || c->peer));
 }
 constexpr size_t kTailRelayBytes = 64 * sizeof(zk::RPost);  // 64 relay slots (k_gkr_tail: RWait, k_gkr_dtail: RPost)
 inline size_t tail_bytes(uint64_t h0) { return kTailRelayBytes + 16 * h0 * sizeof(Fe); }

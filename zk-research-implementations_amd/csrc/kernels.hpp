@@ -226,6 +226,23 @@ __device__ __forceinline__ Fe fold2c(const Fe& x00, const Fe& x01, const Fe& x10
 
 constexpr int kSlotU64 = 256;  // per-block partial slot: up to 256 limb sums (2 KiB)
 
+// Peer reduction (zk_ctx_attach_peer_reduce): the block that publishes a
+// step's sums writes them straight into every rank's receive buffer (an
+// uncached device allocation, IPC-mapped into each peer) and sums the world's
+// contributions itself — the sharded step's all-reduce without an RCCL launch
+// or a publish kernel. Receive buffer: [2 parities][world][kPeerSlotU64] u64,
+// the slot's last word its sequence tag (the same on every rank: one per
+// reduction, in schedule order). Parity (seq & 1) double-buffers the slots:
+// a rank can only send reduction seq once it has every rank's seq - 1, which
+// each rank sends after it has finished reading seq - 2 (the same parity).
+constexpr uint32_t kPeerMax = 8;        // ranks of one node
+constexpr uint32_t kPeerSlotU64 = 512;  // up to kSlotU64 sums, tag in the last word
+constexpr uint64_t kPeerWaitTicks = 1000000000ull;  // 10 s of s_memrealtime: then flag an error and go on
+struct PeerSlots {
+  uint64_t* slot[kPeerMax];  // rank r's receive buffer as mapped in this process (slot[rank]: our own)
+  uint32_t world, rank;
+};
+
 struct RoundSink {
   uint64_t* partials;   // [gridDim.x + 8][kSlotU64]: one slot per block, then 8 shard slots
   uint32_t* counter;    // 9 counters, 128 B apart: 8 XCD shards + top; zero at launch, reset by their last user
@@ -237,6 +254,9 @@ struct RoundSink {
   uint64_t* trace;      // debug (ZK_DEBUG_TAIL): 4 s_memrealtime stamps per tag (entry, challenge, publish), or null
   uint64_t* btrace;     // debug (ZK_DEBUG_BLOCKS): 8 words per block (stamps: main loop end, fan-in start, counted in; chunk count; flushed, words), or null
   uint32_t atomic_max;  // grids up to this many blocks fan in through u64 atomics (ZK_ATOMIC_FANIN)
+  const PeerSlots* peer;  // sums across ranks through the peers' receive buffers, or null
+  uint64_t peer_seq;      // this reduction's sequence tag (peer != null)
+  uint32_t* err;          // pinned error word (a peer that never arrives), or null
 };
 #define ZK_BLOCK_STAMP(sk, i) \
   do { if ((sk).btrace && threadIdx.x == 0 && blockIdx.x < 8192) (sk).btrace[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -381,12 +401,52 @@ __device__ __forceinline__ void block_limb_sums(const Fe& x, Sc& sc, int base) {
 // sc0 sc1) stores — plain stores to the pinned page would sit in L2 — drain,
 // then lane 0 raises the flag. No L2 writeback (buffer_wbl2) is needed since
 // nothing the host reads was written with plain stores.
+// The world's sum of this rank's value v (threads < C; the publishing waves
+// only: wave 0 when C <= 64, else the whole block). Stores and polls are
+// system-scope (sc0 sc1: they bypass the caches), and every store has
+// drained before the tag that announces it is written.
+template <int C>
+__device__ __forceinline__ uint64_t peer_allreduce(uint64_t v, const RoundSink& sk) {
+  const uint32_t t = threadIdx.x;
+  const PeerSlots* ps = sk.peer;
+  const uint32_t W = ps->world, me = ps->rank;
+  const uint64_t par = sk.peer_seq & 1u;
+  const uint64_t mine = (par * W + me) * kPeerSlotU64;
+  if (t < (uint32_t)C)
+    for (uint32_t r = 0; r < W; ++r) __hip_atomic_store(ps->slot[r] + mine + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (C > 64) __syncthreads();  // every storing wave has drained before the tags
+  if (t == 0)
+    for (uint32_t r = 0; r < W; ++r)
+      __hip_atomic_store(ps->slot[r] + mine + kPeerSlotU64 - 1, sk.peer_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint64_t* own = ps->slot[me];
+  if (t < W) {  // lane r waits for rank r's tag
+    const uint64_t* tag = own + (par * W + t) * kPeerSlotU64 + kPeerSlotU64 - 1;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != sk.peer_seq) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerWaitTicks) {
+        if (sk.err) __hip_atomic_store(sk.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  if (C > 64) __syncthreads();  // (C <= 64: wave 0 alone, reconverged after the polls)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the polls
+  uint64_t s = 0;
+  if (t < (uint32_t)C)
+    for (uint32_t r = 0; r < W; ++r) s += __hip_atomic_load(own + (par * W + r) * kPeerSlotU64 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return s;
+}
+
 template <int C, class Sc>
 __device__ __forceinline__ void publish_limbs(Sc& sc, const RoundSink& sk) {
   const uint32_t t = threadIdx.x;
   if (C <= 64 && t >= 64) return;  // wave 0 alone
+  uint64_t pv = 0;
+  if (sk.peer) pv = peer_allreduce<C>(t < (uint32_t)C ? sc.tot[t] : 0, sk);
   if (t < (uint32_t)C) {
-    const uint64_t v = sc.tot[t];
+    const uint64_t v = sk.peer ? pv : sc.tot[t];
     if (sk.dev_out) sk.dev_out[t] = v;
     if (sk.host_out) __hip_atomic_store(sk.host_out + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }

@@ -119,6 +119,7 @@ void zk_ctx_destroy(zk_ctx* c) {
   if (c->h_red) (void)hipHostFree(c->h_red);
   if (c->h_tab) (void)hipHostFree(c->h_tab);
   if (c->h_fslog) (void)hipHostFree(c->h_fslog);
+  peer_release(c);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -638,6 +639,7 @@ int zk_ctx_attach_rccl(zk_ctx* c, int rank, int world, const uint8_t unique_id[1
 int zk_ctx_detach_comm(zk_ctx* c) {
   return guarded([&] {
     require(c, "null ctx");
+    peer_release(c);
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
     c->nccl = nullptr;
     c->rank = 0;
@@ -657,6 +659,19 @@ int zk_ctx_comm_count(const zk_ctx* c, int* out_kind, int* out_rank, int* out_co
     *out_kind = static_cast<int>(c->comm);
     *out_rank = r;
     *out_count = n;
+  });
+}
+int zk_ctx_attach_peer_reduce(zk_ctx* c, int enable, int* out_ok) {
+  return guarded([&] {
+    require(c, "null ctx");
+    if (out_ok) *out_ok = 0;
+    bind(c);
+    peer_release(c);
+    if (!enable) return;
+    require(c->comm != COMM_NONE, "attach a communicator first");
+    require(c->world <= (int)zk::kPeerMax, "peer reduction joins at most 8 ranks (one node)");
+    peer_attach(c);
+    if (out_ok) *out_ok = 1;
   });
 }
 int zk_dev_gkr_sumcheck_prove_sharded(zk_ctx* c, zk_field field, const void* const d_local_tables[4],

@@ -17,7 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-ABI_VERSION = 13  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
+ABI_VERSION = 14  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
 KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33", "coll"]
 
 
@@ -113,6 +113,7 @@ SIGNATURES = {
     "zk_ctx_attach_rccl": (I, [P, I, I, P]),
     "zk_ctx_detach_comm": (I, [P]),
     "zk_ctx_comm_count": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+    "zk_ctx_attach_peer_reduce": (I, [P, I, C.POINTER(I)]),
     "zk_dev_gkr_sumcheck_prove_sharded": (I, [P, I, P, U32, I, P, P, P, P, P]),
 }
 

@@ -21,6 +21,7 @@ class Context:
         self.h = h
         self.device = device
         self._callbacks = None  # keep ctypes callbacks alive while attached
+        self.peer_reduce = False  # zk_ctx_attach_peer_reduce succeeded
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -112,6 +113,19 @@ class Context:
     def detach_comm(self) -> None:
         check(lib().zk_ctx_detach_comm(self.h))
         self._callbacks = None
+        self.peer_reduce = False
+
+    def attach_peer_reduce(self, enable: bool = True) -> None:
+        """Collective (every rank, after attaching a communicator, world <= 8):
+        the sharded steps' sums meet in the ranks' IPC-mapped receive buffers,
+        summed by the step kernels themselves, instead of an all-reduce on the
+        communicator (which still carries the gather). Checked once across
+        the world on attach; raises ZkError if a buffer cannot be opened or the
+        check fails (the context then keeps the communicator's all-reduce)."""
+        ok = C.c_int(0)
+        self.peer_reduce = False
+        check(lib().zk_ctx_attach_peer_reduce(self.h, 1 if enable else 0, C.byref(ok)))
+        self.peer_reduce = bool(ok.value)
 
     def comm_info(self) -> dict:
         """{"kind": "none"|"host"|"rccl", "rank": r, "count": n}; for RCCL the
