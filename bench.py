@@ -53,11 +53,11 @@ def parse():
                     "on one card, a gloo host all-reduce with every rank on device LOCAL_RANK %% device_count")
     ap.add_argument("--force-rccl", action="store_true",
                     help="diagnostic: at world 1 route every step through ncclAllReduce (the multi-rank data path)")
-    ap.add_argument("--reduce", default="rccl", choices=["rccl", "peer"],
+    ap.add_argument("--reduce", default="comm", choices=["comm", "peer"],
                     help="N>1 (or --force-rccl): each step's sums through an all-reduce on the communicator (default) "
                     "or through the ranks' IPC-mapped peer buffers, summed by the step kernels (zk_ctx_attach_peer_reduce)")
     ap.add_argument("--no-peer-leg", action="store_true",
-                    help="N>1 over RCCL: skip the side leg that reruns the headline with --reduce peer in fresh ranks")
+                    help="N>1: skip the side leg that reruns the headline with --reduce peer in fresh ranks")
     ap.add_argument("--no-events", action="store_true", help="diagnostic: time without per-launch HIP events")
     ap.add_argument("--no-plain", action="store_true",
                     help="skip BASELINE config 1 (12-var plain prove, CPU port) and the GPU plain prove/verify legs")
@@ -887,14 +887,14 @@ def main() -> None:
             traffic_src = f"profiles/{os.path.basename(tpath)} ({t['method']}); traffic/alg = {t['traffic_over_alg']:.4f}"
     cfg4 = config4_bench(ctx, field, world, rank, barrier) if args.config4 else None
     peer_leg = None
-    if world > 1 and args.comm == "rccl" and args.reduce == "rccl" and not args.no_peer_leg:
+    if world > 1 and args.reduce == "comm" and not args.no_peer_leg:
         # the headline again with --reduce peer, in N fresh ranks that rank 0
         # starts as child processes (one per GPU): a failure or hang there can
         # only cost the side field, never this line
         if rank == 0:
             cmd = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", str(world), "--steps", str(args.steps),
                    "--warmup", str(args.warmup), "--nvars", str(args.nvars), "--field", args.field, "--seed",
-                   str(args.seed), "--reduce", "peer", "--no-config4", "--no-peer-leg"]
+                   str(args.seed), "--comm", args.comm, "--reduce", "peer", "--no-config4", "--no-peer-leg"]
             t_leg = time.perf_counter()
             rc, text = spawn_ranks(world, cmd, timeout_s=300.0)
             lines = [ln for ln in text.splitlines() if ln.strip()]
@@ -906,7 +906,7 @@ def main() -> None:
                                      "reduce": r.get("reduce"), "comm": r.get("comm"),
                                      "collectives_per_step": r["breakdown_per_step"]["collectives"],
                                      "launches_of_proof": r["roofline"]["launches_of_proof"],
-                                     "vs_rccl": r["value"] / value})
+                                     "vs_comm_reduce": r["value"] / value})
                 except (ValueError, KeyError) as e:
                     peer_leg["error"] = f"unreadable result line: {e}"
             else:
