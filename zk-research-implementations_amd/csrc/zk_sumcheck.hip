@@ -598,6 +598,7 @@ int zk_ctx_attach_host_comm(zk_ctx* c, int rank, int world, zk_allreduce_u64_fn 
     require(c && allreduce, "null argument");
     require(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
     require(rank >= 0 && rank < world, "rank out of range");
+    peer_release(c);  // (a new communicator: the peer buffers are re-attached over it)
     if (c->nccl) {
       (void)ncclCommDestroy(c->nccl);
       c->nccl = nullptr;
@@ -624,6 +625,7 @@ int zk_ctx_attach_rccl(zk_ctx* c, int rank, int world, const uint8_t unique_id[1
     require(world >= 1 && (world & (world - 1)) == 0, "world must be a power of two");
     require(rank >= 0 && rank < world, "rank out of range");
     bind(c);
+    peer_release(c);
     if (c->nccl) {
       (void)ncclCommDestroy(c->nccl);
       c->nccl = nullptr;

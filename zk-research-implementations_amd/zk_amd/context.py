@@ -94,6 +94,7 @@ class Context:
     # ---- communicators ----
     def attach_rccl(self, rank: int, world: int, unique_id: bytes) -> None:
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        self.peer_reduce = False  # (a new communicator releases the peer buffers)
         check(lib().zk_ctx_attach_rccl(self.h, rank, world, buf))
 
     def attach_host_comm(self, rank: int, world: int, allreduce) -> None:
@@ -107,6 +108,7 @@ class Context:
                 return 1
 
         cb = _lib.ALLREDUCE_FN(_ar)
+        self.peer_reduce = False
         check(lib().zk_ctx_attach_host_comm(self.h, rank, world, cb, None))
         self._callbacks = cb
 
