@@ -392,10 +392,12 @@ int zk_ctx_comm_count(const zk_ctx* ctx, int* out_kind, int* out_rank, int* out_
  * checked across the world. From then on each sharded step's sums are
  * summed by the step kernel itself — its publishing block writes them into
  * every rank's buffer and waits for the others' (replacing the step's
- * all-reduce of sum_check_protocol.rs:96-108's round sums; the gather stays on
- * the communicator). enable = 0 releases it. Proofs must then run in the same
- * order on every rank (the reductions carry a shared sequence number); a proof
- * that fails mid-way leaves the sequence unusable until the next attach.
+ * all-reduce of sum_check_protocol.rs:96-108's round sums; the early gather of
+ * <= 4 x 2^12 elements per rank goes through a second such buffer).
+ * enable = 0 releases it, as does attaching a communicator again. Proofs must
+ * then run in the same order on every rank (the reductions carry a shared
+ * sequence number); a proof that fails mid-way leaves the sequence unusable
+ * until the next attach.
  * *out_ok (may be null) = 1 when enabled and the check passed. */
 int zk_ctx_attach_peer_reduce(zk_ctx* ctx, int enable, int* out_ok);
 /* gkr_prove over the global (nvars_local + log2(world))-variable SumPoly whose

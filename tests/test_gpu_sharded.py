@@ -168,8 +168,11 @@ def test_config4_workload_8_ranks_matches_fixture(tmp_path):
 # (host communicator for the handle exchange and the gather; steps launch after
 # their challenges); at world 1 over RCCL (ZK_FORCE_COLLECTIVES=1) it runs the
 # product schedule: pre-enqueued steps, no RCCL all-reduce or publish kernel.
+# (gather <= 12 local variables: the early gather goes through the peers' gather
+# buffers too, k_peer_gather; 14: it falls back to the communicator's)
 @pytest.mark.parametrize("world,nloc,field,gather", [(2, 12, 0, "10"), (2, 16, 2, "0"), (4, 13, 1, "6"), (8, 14, 0, "10"),
-                                                     (8, 10, 2, "0"), (2, 20, 0, "10"), (4, 0, 0, "10")])
+                                                     (8, 10, 2, "0"), (2, 20, 0, "10"), (4, 0, 0, "10"), (2, 18, 0, "14"),
+                                                     (4, 14, 0, "12")])
 def test_peer_reduce_ranks_match_single_process(tmp_path, world, nloc, field, gather):
     res = _run(world, "host", field, nloc, str(tmp_path), {"PEER": "1", "ZK_GATHER_VARS": gather})
     want = _oracle(field, nloc + world.bit_length() - 1)

@@ -246,6 +246,7 @@ struct zk_ctx {
   // in the ranks' IPC-mapped receive buffers instead of an RCCL all-reduce
   bool peer = false;
   uint64_t* peer_buf = nullptr;       // our receive buffer (uncached device memory)
+  uint64_t* peer_gbuf = nullptr;      // our early-gather receive buffer (uncached): [world][4 x 2^12 Fe], world tags
   std::vector<void*> peer_open;       // the peers' buffers, opened from their IPC handles
   zk::PeerSlots* d_peer = nullptr;    // device copy of the slot table
   uint64_t peer_seq = 0;              // last reduction's sequence tag (the same on every rank)
@@ -457,8 +458,10 @@ inline void peer_release(zk_ctx* c) {
   c->peer_open.clear();
   if (c->d_peer) (void)hipFree(c->d_peer);
   if (c->peer_buf) (void)hipFree(c->peer_buf);
+  if (c->peer_gbuf) (void)hipFree(c->peer_gbuf);
   c->d_peer = nullptr;
   c->peer_buf = nullptr;
+  c->peer_gbuf = nullptr;
   c->peer = false;
   c->peer_seq = 0;
 }
@@ -473,16 +476,57 @@ static __global__ void k_peer_check(zk::RoundSink sk) {
   zk::publish_limbs<16>(sc, sk);
 }
 
+// The early gather through the peers: one block copies this rank's slot (n
+// u64) into every rank's gather buffer at [rank] with system-scope stores,
+// drains, raises its tag there, then waits until every rank's tag has arrived
+// in its own buffer (k_interleave then reads it like the communicator's).
+static __global__ __launch_bounds__(1024) void k_peer_gather(const zk::PeerSlots* __restrict__ ps, const uint64_t* __restrict__ src,
+                                                      uint64_t n, uint64_t seq, uint32_t* err) {
+  const uint32_t t = threadIdx.x, W = ps->world, me = ps->rank;
+  const uint64_t cap = (uint64_t)4 * (1u << zk::kPeerGatherMaxT) * 4;  // u64 per rank slot
+  for (uint32_t r = 0; r < W; ++r) {
+    uint64_t* dst = ps->gather[r] + me * cap;
+    for (uint64_t i = t; i < n; i += blockDim.x) __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    for (uint32_t r = 0; r < W; ++r)
+      __hip_atomic_store(ps->gather[r] + W * cap + me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < W) {
+    const uint64_t* tag = ps->gather[me] + W * cap + t;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > zk::kPeerWaitTicks) {
+        __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+}
+
+// (launched through this non-template wrapper: every unit that includes the kernel uses it)
+inline void launch_peer_gather(zk_ctx* c, const void* src, uint64_t n) {
+  k_peer_gather<<<1, 1024, 0, c->stream>>>(c->d_peer, reinterpret_cast<const uint64_t*>(src), n, ++c->peer_seq, h_err(c));
+  HIPCK(hipGetLastError());
+}
+inline size_t peer_gather_bytes(int world) {
+  return ((size_t)world * 4 * ((size_t)1 << zk::kPeerGatherMaxT) * 4 + zk::kPeerMax) * sizeof(uint64_t);
+}
 inline void peer_attach(zk_ctx* c) {
-  const size_t bytes = 2 * (size_t)c->world * zk::kPeerSlotU64 * sizeof(uint64_t);
+  const size_t bytes = 2 * (size_t)c->world * zk::kPeerSlotU64 * sizeof(uint64_t), gbytes = peer_gather_bytes(c->world);
   HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_buf), bytes, hipDeviceMallocUncached));
+  HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_gbuf), gbytes, hipDeviceMallocUncached));
   HIPCK(hipMemset(c->peer_buf, 0, bytes));
+  HIPCK(hipMemset(c->peer_gbuf, 0, gbytes));
   HIPCK(hipDeviceSynchronize());
-  hipIpcMemHandle_t h;
-  HIPCK(hipIpcGetMemHandle(&h, c->peer_buf));
-  constexpr size_t HW = (sizeof(hipIpcMemHandle_t) + 7) / 8;
+  hipIpcMemHandle_t h[2];
+  HIPCK(hipIpcGetMemHandle(&h[0], c->peer_buf));
+  HIPCK(hipIpcGetMemHandle(&h[1], c->peer_gbuf));
+  constexpr size_t HW = (2 * sizeof(hipIpcMemHandle_t) + 7) / 8;
   std::vector<uint64_t> w(HW * c->world, 0);
-  memcpy(&w[HW * c->rank], &h, sizeof h);
+  memcpy(&w[HW * c->rank], h, sizeof h);
   allreduce_host(c, w.data(), w.size());  // disjoint slots: the sum is the gather
   zk::PeerSlots ps{};
   ps.world = (uint32_t)c->world;
@@ -490,18 +534,21 @@ inline void peer_attach(zk_ctx* c) {
   for (int r = 0; r < c->world; ++r) {
     if (r == c->rank) {
       ps.slot[r] = c->peer_buf;
+      ps.gather[r] = c->peer_gbuf;
       continue;
     }
-    hipIpcMemHandle_t hr;
-    memcpy(&hr, &w[HW * r], sizeof hr);
-    void* p = nullptr;
-    const hipError_t e = hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) {
-      peer_release(c);
-      fail(ZK_ECOMM, std::string("peer reduction: opening rank ") + std::to_string(r) + "'s buffer: " + hipGetErrorString(e));
+    hipIpcMemHandle_t hr[2];
+    memcpy(hr, &w[HW * r], sizeof hr);
+    for (int b = 0; b < 2; ++b) {
+      void* p = nullptr;
+      const hipError_t e = hipIpcOpenMemHandle(&p, hr[b], hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        peer_release(c);
+        fail(ZK_ECOMM, std::string("peer reduction: opening rank ") + std::to_string(r) + "'s buffer: " + hipGetErrorString(e));
+      }
+      c->peer_open.push_back(p);
+      (b == 0 ? ps.slot[r] : ps.gather[r]) = reinterpret_cast<uint64_t*>(p);
     }
-    c->peer_open.push_back(p);
-    ps.slot[r] = reinterpret_cast<uint64_t*>(p);
   }
   HIPCK(hipMalloc(reinterpret_cast<void**>(&c->d_peer), sizeof ps));
   HIPCK(hipMemcpy(c->d_peer, &ps, sizeof ps, hipMemcpyHostToDevice));
@@ -1557,7 +1604,8 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
     Fe* sc = reinterpret_cast<Fe*>(c->gbuf.p);
     Fe* oh = sc + scratch;
     Fe* gl = oh + onehot;
-    if (c->comm != COMM_RCCL) HIPCK(hipMemsetAsync(oh, 0, onehot * sizeof(Fe), c->stream));
+    const bool via_peer = c->peer && T <= zk::kPeerGatherMaxT;
+    if (c->comm != COMM_RCCL && !via_peer) HIPCK(hipMemsetAsync(oh, 0, onehot * sizeof(Fe), c->stream));
     Fe* slot = oh + (size_t)c->rank * 4 * Tn;
     if (pend == 0) {
       for (int t = 0; t < 4; ++t) HIPCK(hipMemcpyAsync(slot + t * Tn, cur[t], Tn * 32, hipMemcpyDeviceToDevice, c->stream));
@@ -1571,7 +1619,18 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
              cur[2], cur[3], dst, dst + dstride, dst + 2 * dstride, dst + 3 * dstride, half, rj);
       for (int t = 0; t < 4; ++t) cur[t] = dst + t * dstride;
     }
-    if (c->comm == COMM_RCCL) {  // in place: this rank's slot is its send buffer
+    const Fe* gsrc = oh;
+    if (via_peer) {  // through the peers' gather buffers (k_peer_gather)
+      const uint64_t cap = (uint64_t)4 * ((uint64_t)1 << zk::kPeerGatherMaxT);  // elements per rank slot
+      launch_peer_gather(c, slot, 4 * Tn * 4);
+      c->stats.collectives += 1;
+      if (cap != 4 * Tn) {  // [G][cap] -> [G][4 Tn]: the layout k_interleave reads
+        HIPCK(hipMemcpy2DAsync(oh, 4 * Tn * sizeof(Fe), c->peer_gbuf, cap * sizeof(Fe), 4 * Tn * sizeof(Fe), (size_t)G,
+                               hipMemcpyDeviceToDevice, c->stream));
+      } else {
+        gsrc = reinterpret_cast<const Fe*>(c->peer_gbuf);
+      }
+    } else if (c->comm == COMM_RCCL) {  // in place: this rank's slot is its send buffer
       CollTimer ct(c, 4.0 * Tn * 32);
       NCCLCK(ncclAllGather(slot, oh, (size_t)4 * Tn * 4, ncclUint64, c->nccl, c->stream));
       c->stats.collectives += 1;
@@ -1583,8 +1642,9 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
       HIPCK(hipMemcpyAsync(oh, w.data(), onehot * sizeof(Fe), hipMemcpyHostToDevice, c->stream));
       sync(c);  // w (pageable) is released at the end of this block
     }
-    launch(c, ZK_K_FOLD, global * 64.0, 0.0, zk::k_interleave<F>, grid_for(c, global, zk::k_interleave<F>), (const Fe*)oh, gl,
+    launch(c, ZK_K_FOLD, global * 64.0, 0.0, zk::k_interleave<F>, grid_for(c, global, zk::k_interleave<F>), gsrc, gl,
            Tn, (uint32_t)G);
+    if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) == 2u) fail(ZK_EDEVICE, "a peer's gather slot never arrived (10 s)");
     const Fe* gcur[4] = {gl, gl + G * Tn, gl + 2 * G * Tn, gl + 3 * G * Tn};
     gkr_phase<F>(c, gcur, T + lg, stop, false, tr, out, claim, r, pend, true);
     sync(c);

@@ -238,10 +238,13 @@ constexpr int kSlotU64 = 256;  // per-block partial slot: up to 256 limb sums (2
 constexpr uint32_t kPeerMax = 8;        // ranks of one node
 constexpr uint32_t kPeerSlotU64 = 512;  // up to kSlotU64 sums, tag in the last word
 constexpr uint64_t kPeerWaitTicks = 1000000000ull;  // 10 s of s_memrealtime: then flag an error and go on
+constexpr uint32_t kPeerGatherMaxT = 12;  // the early gather through the peers up to 4 x 2^12 elements per rank
 struct PeerSlots {
-  uint64_t* slot[kPeerMax];  // rank r's receive buffer as mapped in this process (slot[rank]: our own)
+  uint64_t* slot[kPeerMax];    // rank r's receive buffer as mapped in this process (slot[rank]: our own)
+  uint64_t* gather[kPeerMax];  // rank r's gather buffer: [world][4 x 2^kPeerGatherMaxT elements], then world tags
   uint32_t world, rank;
 };
+
 
 struct RoundSink {
   uint64_t* partials;   // [gridDim.x + 8][kSlotU64]: one slot per block, then 8 shard slots
