@@ -896,7 +896,7 @@ def main() -> None:
                    "--warmup", str(args.warmup), "--nvars", str(args.nvars), "--field", args.field, "--seed",
                    str(args.seed), "--comm", args.comm, "--reduce", "peer", "--no-config4", "--no-peer-leg"]
             t_leg = time.perf_counter()
-            rc, text = spawn_ranks(world, cmd, timeout_s=300.0)
+            rc, text = spawn_ranks(world, cmd, timeout_s=180.0)
             lines = [ln for ln in text.splitlines() if ln.strip()]
             peer_leg = {"cmd": " ".join(cmd[2:]), "rc": rc, "wall_s": round(time.perf_counter() - t_leg, 1)}
             if rc == 0 and lines:
