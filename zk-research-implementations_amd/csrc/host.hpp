@@ -1644,7 +1644,8 @@ void gkr_prove_device(zk_ctx* c, const Fe* const dT[4], uint32_t nloc, bool shar
     }
     launch(c, ZK_K_FOLD, global * 64.0, 0.0, zk::k_interleave<F>, grid_for(c, global, zk::k_interleave<F>), gsrc, gl,
            Tn, (uint32_t)G);
-    if (__atomic_load_n(h_err(c), __ATOMIC_ACQUIRE) == 2u) fail(ZK_EDEVICE, "a peer's gather slot never arrived (10 s)");
+    // (a peer gather slot that never arrives sets the error word: the next
+    // step's collect_sums reports it)
     const Fe* gcur[4] = {gl, gl + G * Tn, gl + 2 * G * Tn, gl + 3 * G * Tn};
     gkr_phase<F>(c, gcur, T + lg, stop, false, tr, out, claim, r, pend, true);
     sync(c);
