@@ -165,6 +165,17 @@ template <class F>
 inline Fe hfe_sub(const Fe& a, const Fe& b) {
   return h64::fe(h64::sub<F>(h64::of(a), h64::of(b)));
 }
+// x / 2 mod p (x < p; Montgomery-linear: the image of x/2 is half the image of x)
+template <class F>
+inline Fe hfe_half(const Fe& x) {
+  h64::V v = h64::of(x);
+  const uint64_t odd = (uint64_t)0 - (v.l[0] & 1);
+  unsigned long c = 0;
+  for (int i = 0; i < 4; ++i) v.l[i] = __builtin_addcl(v.l[i], h64::P<F>(i) & odd, c, &c);  // < 2p < 2^256
+  for (int i = 0; i < 3; ++i) v.l[i] = (v.l[i] >> 1) | (v.l[i + 1] << 63);
+  v.l[3] >>= 1;
+  return h64::fe(v);
+}
 template <class F>
 inline Fe hfe_from_mont(const Fe& m) {
   h64::V one = {{1, 0, 0, 0}};
@@ -177,6 +188,18 @@ inline Fe hfe_to_mont(const Fe& canon_any) {  // any 256-bit value, reduced mod 
 // limbs_to_fe (field.hpp) on 64-bit limbs
 template <class F>
 inline Fe hlimbs_to_fe(const uint64_t* w, int L, bool product) {
+  if (product && L <= 9) {  // the matrix-core steps' 9 limb sums: T < 2^320 < p R, one REDC
+    using u128 = unsigned __int128;
+    uint64_t t8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u128 acc = 0;
+    for (int k = 0; k < 5; ++k) {
+      acc += (u128)(2 * k < L ? w[2 * k] : 0) + ((u128)(2 * k + 1 < L ? w[2 * k + 1] : 0) << 32);
+      t8[k] = (uint64_t)acc;
+      acc >>= 64;
+    }
+    t8[5] = (uint64_t)acc;
+    return h64::fe(h64::redc512<F>(t8));
+  }
   // T = sum_i w[i] 2^(32 i): add the even words and the odd words shifted by
   // 32 into 64-bit limbs with carries
   uint64_t t[13] = {0};

@@ -690,7 +690,7 @@ Fe finish_round(zk_transcript* tr, const Fe& e0, const Fe& e1, const Fe& e2, uin
   using namespace zk;
   Fe c[3];
   c[0] = e0;
-  c[2] = hfe_mul<F>(hfe_add<F>(hfe_sub<F>(e0, hfe_add<F>(e1, e1)), e2), fe_inv2<F>());
+  c[2] = hfe_half<F>(hfe_add<F>(hfe_sub<F>(e0, hfe_add<F>(e1, e1)), e2));
   c[1] = hfe_sub<F>(hfe_sub<F>(e1, e0), c[2]);
   int m = 3;
   while (m > 0 && fe_is_zero<F>(c[m - 1])) --m;
@@ -1250,12 +1250,18 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     if (nx.kind == GS_T32 || nx.kind == GS_T33) {
       // eq((rz, ra, rb), c), c = 4a + 2b + c0 (rz, the oldest, on the top bit): the
       // fold's eight weights, formed here instead of in every block of the step
+      // (five products: ab = eq((rz, ra), (a, b)) from rz ra by differences,
+      // then e(ab, c = 1) = ab rb and e(ab, c = 0) = ab - ab rb)
       const Fe one = zk::fe_one<F>();
+      Fe ab[4];
+      ab[3] = zk::hfe_mul<F>(rz, ra);
+      ab[2] = zk::hfe_sub<F>(rz, ab[3]);                          // rz (1 - ra)
+      ab[1] = zk::hfe_sub<F>(ra, ab[3]);                          // (1 - rz) ra
+      ab[0] = zk::hfe_sub<F>(zk::hfe_sub<F>(one, rz), ab[1]);     // (1 - rz)(1 - ra)
       Fe e[8];
-      for (int q = 0; q < 8; ++q) {
-        const Fe fa = (q & 4) ? rz : zk::hfe_sub<F>(one, rz), fb = (q & 2) ? ra : zk::hfe_sub<F>(one, ra);
-        const Fe fc = (q & 1) ? rb : zk::hfe_sub<F>(one, rb);
-        e[q] = zk::hfe_mul<F>(zk::hfe_mul<F>(fa, fb), fc);
+      for (int q = 0; q < 4; ++q) {
+        e[2 * q + 1] = zk::hfe_mul<F>(ab[q], rb);
+        e[2 * q] = zk::hfe_sub<F>(ab[q], e[2 * q + 1]);
       }
       post.post8(e, rtags[si + 1]);
     } else if (nx.kind == GS_DTAIL && nx.dfs) {
@@ -1291,15 +1297,15 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     Fe T[zk::kD0TCats];
     collect_sums<F, zk::kD0TCats>(c, sinks[i0], across_ranks, 9, T, true);
     using namespace zk;
-    const Fe one = fe_one<F>(), two = hfe_add<F>(one, one), four = hfe_add<F>(two, two);
-    auto at2w = [&](const Fe& m0, const Fe& m1, const Fe& ms) {  // value at t = 2
-      return hfe_sub<F>(hfe_add<F>(m0, hfe_mul<F>(four, m1)), hfe_mul<F>(two, ms));
+    const Fe one = fe_one<F>();
+    auto at2w = [&](const Fe& m0, const Fe& m1, const Fe& ms) {  // value at t = 2: m0 + 4 m1 - 2 ms
+      const Fe m1x2 = hfe_add<F>(m1, m1);
+      return hfe_sub<F>(hfe_add<F>(m0, hfe_add<F>(m1x2, m1x2)), hfe_add<F>(ms, ms));
     };
-    auto wts = [&](const Fe& t, Fe (&w)[3]) {
-      const Fe omt = hfe_sub<F>(one, t);
-      w[0] = hfe_mul<F>(omt, omt);
+    auto wts = [&](const Fe& t, Fe (&w)[3]) {  // (1-t)^2 = (1-t) - t(1-t), t(1-t) = t - t^2
       w[1] = hfe_mul<F>(t, t);
-      w[2] = hfe_mul<F>(t, omt);
+      w[2] = hfe_sub<F>(t, w[1]);
+      w[0] = hfe_sub<F>(hfe_sub<F>(one, t), w[2]);
     };
     Fe U[3];  // round i0: U[alpha] = sum over beta, gamma in {0, 1}
     for (int a = 0; a < 3; ++a)
@@ -1345,11 +1351,11 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       const Fe e1 = first ? zk::hfe_add<F>(d[4], d[8]) : zk::hfe_sub<F>(claim, e0);
       one_round(i0, e0, e1, zk::hfe_add<F>(d[5], d[6]));
       // round i + 1 at r = r_i: e0' through (V00, V10, V20), e2' through (V02, V12, V22) at r = 0, 1, 2
-      const Fe one = zk::fe_one<F>(), two = zk::hfe_add<F>(one, one), h = zk::fe_inv2<F>();
+      const Fe one = zk::fe_one<F>(), two = zk::hfe_add<F>(one, one);
       const Fe rm1 = zk::hfe_sub<F>(r, one), rm2 = zk::hfe_sub<F>(r, two);
-      const Fe L0 = zk::hfe_mul<F>(zk::hfe_mul<F>(rm1, rm2), h);                 // (r-1)(r-2)/2
+      const Fe L0 = zk::hfe_half<F>(zk::hfe_mul<F>(rm1, rm2));                   // (r-1)(r-2)/2
       const Fe L1 = zk::hfe_sub<F>(zk::fe_zero<F>(), zk::hfe_mul<F>(r, rm2));     // -r(r-2)
-      const Fe L2 = zk::hfe_mul<F>(zk::hfe_mul<F>(r, rm1), h);                   // r(r-1)/2
+      const Fe L2 = zk::hfe_half<F>(zk::hfe_mul<F>(r, rm1));                     // r(r-1)/2
       auto lag = [&](const Fe& v0, const Fe& v1, const Fe& v2) {
         return zk::hfe_add<F>(zk::hfe_add<F>(zk::hfe_mul<F>(L0, v0), zk::hfe_mul<F>(L1, v1)), zk::hfe_mul<F>(L2, v2));
       };
