@@ -4,7 +4,9 @@
 //    steps' output) against its generic path (the same words padded to L = 10,
 //    which takes the generic route), on random, small, all-ones and 32-bit words;
 //  * hfe_half against multiplication by 1/2 (finish_round's c2, the Lagrange
-//    weights of two_rounds).
+//    weights of two_rounds);
+//  * wide_to_fe's one-REDC path against the generic conversion (sums of 1-4
+//    products of BLS12-381 Fr elements: 3p^2 exceeds p R there, so both paths run).
 // Prints the time of 27 conversions (one three-round step's worth).
 #include <chrono>
 #include <cstdio>
@@ -52,6 +54,28 @@ int main() {
     x = hfe_to_mont<Bn254Fr>(x);
     const Fe a = hfe_half<Bn254Fr>(x), b = hfe_mul<Bn254Fr>(x, fe_inv2<Bn254Fr>());
     bad += memcmp(&a, &b, sizeof a) != 0;
+  }
+  // wide_to_fe's one-REDC path against the generic conversion of the same 576-bit value
+  for (int it = 0; it < 1000000; ++it) {
+    uint64_t acc[9] = {0};
+    const int np = 1 + it % 4;
+    for (int k = 0; k < np; ++k) {
+      Fe a, b;
+      for (int i = 0; i < 8; ++i) {
+        a.v[i] = (uint32_t)g();
+        b.v[i] = (uint32_t)g();
+      }
+      a = hfe_to_mont<Bls12_381Fr>(a);
+      b = hfe_to_mont<Bls12_381Fr>(b);
+      h64::mac_wide(acc, h64::of(a), h64::of(b));
+    }
+    uint64_t w[18];
+    for (int k = 0; k < 9; ++k) {
+      w[2 * k] = (uint32_t)acc[k];
+      w[2 * k + 1] = acc[k] >> 32;
+    }
+    const Fe x = wide_to_fe<Bls12_381Fr>(acc), y = hlimbs_to_fe<Bls12_381Fr>(w, 18, true);
+    bad += memcmp(&x, &y, sizeof x) != 0;
   }
   printf("total mismatches %d\n", bad);
   return bad != 0;

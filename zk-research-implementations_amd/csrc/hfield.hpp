@@ -233,6 +233,8 @@ inline Fe hlimbs_to_fe(const uint64_t* w, int L, bool product) {
 // sum of products of Montgomery images accumulated by mac_wide -> Montgomery image of the field sum
 template <class F>
 inline Fe wide_to_fe(const uint64_t (&acc)[9]) {
+  if (acc[8] == 0 && h64::lt_p<F>(acc + 4))  // < p R: one REDC (a few products of values < p)
+    return h64::fe(h64::redc512<F>(*reinterpret_cast<const uint64_t(*)[8]>(acc)));
   uint64_t w[18];
   for (int k = 0; k < 9; ++k) {
     w[2 * k] = (uint32_t)acc[k];

@@ -649,6 +649,7 @@ void collect_sums(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int L, 
     fail(ZK_EDEVICE, e == 2u ? "a peer's sums never arrived (peer reduction, 10 s)"
                              : "a pre-enqueued round kernel waited more than 1 s for its challenge");
   uint64_t w[K * 17 > 17 ? K * 17 : 17];
+  for (int i = 0; i < n; i += 8) __builtin_prefetch(c->h_red + i);  // the device wrote these lines: misses in flight together
   for (int i = 0; i < n; ++i) w[i] = __atomic_load_n(c->h_red + i, __ATOMIC_RELAXED);
   if (multi && c->comm == COMM_HOST && !c->peer) {
     CollTimer ct(c, 8.0 * n);
