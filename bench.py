@@ -636,7 +636,12 @@ def spawn_ranks(n: int, cmd: list, env_extra: dict | None = None, grace_s: float
     still running after it are killed and the result is a failure (124)."""
     import signal
 
-    env0 = dict(os.environ)
+    # (a caller that is itself a torch.distributed.run worker — rank 0 starting
+    # the peer-reduction side leg — must not hand its elastic-agent settings
+    # down: with TORCHELASTIC_USE_AGENT_STORE the children would wait for an
+    # agent store on their fresh port instead of hosting their own)
+    drop = ("TORCHELASTIC_", "GROUP_", "ROLE_", "TORCH_ELASTIC")
+    env0 = {k: v for k, v in os.environ.items() if not k.startswith(drop)}
     env0.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
                  "MASTER_PORT": str(_free_port()), "ZK_BENCH_LAUNCHER": "self"})
     env0.update(env_extra or {})

@@ -97,3 +97,19 @@ def test_timeout_does_not_touch_ranks_that_finish():
     code = "import os; print('{\"ok\": 1}') if os.environ['RANK'] == '0' else None"
     rc, text = bench.spawn_ranks(2, [sys.executable, "-c", code], timeout_s=120.0)
     assert rc == 0 and json.loads(text.splitlines()[-1]) == {"ok": 1}
+
+
+def test_elastic_agent_settings_are_not_inherited(monkeypatch):
+    """Rank 0 of a torch.distributed.run job starts the peer-reduction side leg
+    through spawn_ranks: its children must host their own rendezvous store,
+    so the elastic agent's variables (TORCHELASTIC_USE_AGENT_STORE above all)
+    are not passed down."""
+    monkeypatch.setenv("TORCHELASTIC_USE_AGENT_STORE", "True")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    monkeypatch.setenv("GROUP_WORLD_SIZE", "1")
+    monkeypatch.setenv("ROLE_RANK", "3")
+    code = ("import os, json; print(json.dumps(sorted(k for k in os.environ if k.startswith("
+            "('TORCHELASTIC_', 'GROUP_WORLD', 'ROLE_')))))")
+    rc, text = bench.spawn_ranks(2, [sys.executable, "-c", code])
+    assert rc == 0
+    assert json.loads(text.splitlines()[-1]) == []
