@@ -110,6 +110,29 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
 // many threads run (2 waves per SIMD of a 256-CU MI355X)
 constexpr uint64_t kMsmMinThreads = 1u << 17;
 
+// window width of a c-bit signed-digit Pippenger (msm_g1_device). The window
+// sums cost ~0.9-2 ns per bucket against ~0.21 ns per bucket-sum entry (round 5
+// rocprof of get_proof's MSMs): kBucketCost 5.
+constexpr double kBucketCost = 5.0;
+inline uint32_t msm_window_bits(uint64_t n, uint32_t lg) {
+  if (const char* e = getenv("ZK_MSM_C")) {  // (diagnostic) a fixed width, 6..20
+    const uint32_t f = (uint32_t)strtoul(e, nullptr, 0);
+    if (f >= 6 && f <= 20) return f;
+  }
+  if (lg < 12) return std::min<uint32_t>(20, std::max<uint32_t>(6, lg > 9 ? lg - 3 : 6));
+  uint32_t best = 16;
+  double best_cost = 1e300;
+  for (uint32_t cc : {8u, 10u, 13u, 16u, 20u}) {
+    const double W = (double)((256 + cc - 1) / cc);
+    const double cost = (double)n * W + kBucketCost * W * (double)(1ull << (cc - 1));
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = cc;
+    }
+  }
+  return best;
+}
+
 // sum_i scalars[i] * bases[i]; scalars canonical Fr (device), bases affine Montgomery (device)
 G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   using namespace zk;
@@ -117,10 +140,14 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   require(n < (1ull << 28), "MSM too large");
   uint32_t lg = 0;
   while ((2ull << lg) <= n) ++lg;
-  // c-bit signed digits (msm.hpp signed_digits): W c >= 256, 2^(c-1) buckets per window
-  // (c = log2 n - 3 in [6, 20], then evened out over its W windows so the top
-  // window is not a sliver: 17 -> 16 x 16 bits, 20 stays 13 x 20)
-  const uint32_t c0 = std::min<uint32_t>(20, std::max<uint32_t>(6, lg > 9 ? lg - 3 : 6));
+  // c-bit signed digits (msm.hpp signed_digits): W c >= 256, 2^(c-1) buckets per window.
+  // Small MSMs: c = log2 n - 3 in [6, 20], evened out over its W windows.
+  // From 2^12 points (c_msm_bits): the width among 8, 10, 13, 16, 20 bits —
+  // the ones whose top window keeps >= 6 bits (19, 18, 15, 14 leave 9, 4, 1, 4:
+  // a sliver sends every point to a handful of buckets, whose long segments
+  // take extra reduction levels) — that minimises n W + kBucketCost W 2^(c-1)
+  // (bucket additions against the window sums' per-bucket cost).
+  const uint32_t c0 = msm_window_bits(n, lg);
   const uint32_t W = (256 + c0 - 1) / c0;
   const uint32_t cb = (256 + W - 1) / W;
   const uint32_t bb = cb - 1;  // bucket key bits
