@@ -161,16 +161,17 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   {  // bucket sort (msm.hpp k_sort_hist / k_sort_scatter / k_sort_fine)
     const uint32_t C = bb - sort_fine_bits(bb), nbin = W << C;
     require(nbin <= kSortBinsMax, "internal: MSM coarse bins exceed the LDS table");
-    const uint32_t NB = (uint32_t)((n + kSortPts - 1) / kSortPts);
+    const uint32_t pts = sort_block_pts(n);
+    const uint32_t NB = (uint32_t)((n + pts - 1) / pts);
     const uint64_t nh = (uint64_t)nbin * NB + 1;
     cur.ensure(nh * 4);
     DevBuf& ent = c->msm[16];
     ent.ensure(std::max<uint64_t>(1, n * W) * 8);
     HIPCK(hipMemsetAsync(cur.p, 0, nh * 4, c->stream));
-    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist, NB, scalars, n, cb, W, NB, dptr<uint32_t>(cur));
+    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist, NB, scalars, n, cb, W, NB, pts, dptr<uint32_t>(cur));
     scan_u32(c, dptr<uint32_t>(cur), nh);
-    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, NB, (const uint32_t*)dptr<uint32_t>(cur),
-           dptr<uint64_t>(ent));
+    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, NB, pts,
+           (const uint32_t*)dptr<uint32_t>(cur), dptr<uint64_t>(ent));
     launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), bb, NB,
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
   }

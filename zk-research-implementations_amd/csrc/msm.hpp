@@ -97,17 +97,23 @@ __device__ __forceinline__ void signed_digits(const Fe& s, uint32_t c, uint32_t 
 // last bits), and low coarse bits spread them over every bin. Buckets are
 // therefore stored at bucket_slot(key) = low << F | high (window sums read
 // them through it):
-//  1. k_sort_hist: block b counts its kSortPts points' entries per (window,
+//  1. k_sort_hist: block b counts its `pts` points' entries per (window,
 //     coarse bin) in LDS and stores the counts bin-major, H[bin NB + b];
 //  2. an exclusive scan of H gives every block its run in every coarse bin;
 //  3. k_sort_scatter: the block writes (point, sign, fine) into its runs (LDS
-//     cursors, runs of ~kSortPts / 2^C entries);
+//     cursors, runs of ~pts / 2^C entries);
 //  4. k_sort_fine: one block per coarse bin counting-sorts its entries by the
 //     fine bits in LDS and writes the bucket offsets (the exclusive scan of the
 //     per-bucket counts, `cnt`) and the point order `ord` (bit 31: negate).
 // Within a bucket the order is arbitrary (LDS atomics): bucket sums are group
 // sums.
-constexpr uint32_t kSortPts = 16384;        // points per block in passes 1 and 3
+// points per block in passes 1 and 3: kSortPts for large MSMs; small ones use
+// fewer (sort_block_pts), so that their passes run on more than a few blocks
+constexpr uint32_t kSortPts = 16384;
+__host__ __device__ __forceinline__ uint32_t sort_block_pts(uint64_t n) {
+  const uint64_t p = (n + 255) / 256;
+  return (uint32_t)(p < 1024 ? 1024 : (p > kSortPts ? kSortPts : p));
+}
 constexpr uint32_t kSortBinsMax = 13312;    // W 2^C over c = 6..20 (c = 20: 13 x 1024)
 __host__ __device__ __forceinline__ uint32_t sort_fine_bits(uint32_t b) { return b / 2; }
 __host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t b) {
@@ -115,12 +121,12 @@ __host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t 
   return ((key & ((1u << C) - 1u)) << F) | (key >> C);
 }
 __global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
-                                                      uint32_t W, uint32_t NB, uint32_t* __restrict__ H) {
+                                                      uint32_t W, uint32_t NB, uint32_t pts, uint32_t* __restrict__ H) {
   __shared__ uint32_t hist[kSortBinsMax];
   const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = W << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) hist[j] = 0;
   __syncthreads();
-  const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
+  const uint64_t p0 = (uint64_t)blockIdx.x * pts, p1 = p0 + pts < n ? p0 + pts : n;
   for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
     signed_digits(ld_fe(scalars, i), c, W,
                   [&](uint32_t w, uint32_t key, uint32_t) { atomicAdd(&hist[(w << C) + (key & ((1u << C) - 1u))], 1u); });
@@ -128,13 +134,13 @@ __global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ sca
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) H[(uint64_t)j * NB + blockIdx.x] = hist[j];
 }
 __global__ __launch_bounds__(kBlock) void k_sort_scatter(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
-                                                         uint32_t W, uint32_t NB, const uint32_t* __restrict__ Hs,
-                                                         uint64_t* __restrict__ E) {
+                                                         uint32_t W, uint32_t NB, uint32_t pts,
+                                                         const uint32_t* __restrict__ Hs, uint64_t* __restrict__ E) {
   __shared__ uint32_t cur[kSortBinsMax];
   const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = W << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) cur[j] = Hs[(uint64_t)j * NB + blockIdx.x];
   __syncthreads();
-  const uint64_t p0 = (uint64_t)blockIdx.x * kSortPts, p1 = p0 + kSortPts < n ? p0 + kSortPts : n;
+  const uint64_t p0 = (uint64_t)blockIdx.x * pts, p1 = p0 + pts < n ? p0 + pts : n;
   for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
     signed_digits(ld_fe(scalars, i), c, W, [&](uint32_t w, uint32_t key, uint32_t neg) {
       const uint32_t pos = atomicAdd(&cur[(w << C) + (key & ((1u << C) - 1u))], 1u);
