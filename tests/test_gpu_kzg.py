@@ -296,3 +296,27 @@ def test_get_proof_large_window_verifies(ctx):
     assert not KZG.verify(c, (v + 1) % R, proof, point, k.g2_taus)
     assert not KZG.verify(c, v, proof[1:] + proof[:1], point, k.g2_taus)
     k.close()
+
+
+@pytest.mark.parametrize("batch", ["0", "1", "6", "14"])
+def test_get_proof_level_batched_quotients(ctx, monkeypatch, batch):
+    """kzg_get_proof commits its last ZK_PROOF_BATCH_LEVELS quotients (14 by
+    default: <= 2^13 points each) in one level-batched MSM pass (msm_levels:
+    level v = points [2^v - 1, 2^(v+1) - 1) of the suffix bases, its own W
+    windows); every split gives the per-level proof, and each element equals
+    q_i(taus) * G1 (16 variables: two levels committed alone at 14)."""
+    rng = random.Random(31)
+    n = 16
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)]
+    point = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    v = k.open(point, evals)
+    monkeypatch.setenv("ZK_PROOF_BATCH_LEVELS", batch)
+    proof = k.get_proof(v, point, evals)
+    cur = [(e - v) % R for e in evals]
+    for i in range(n):
+        q = ko.get_quotient(cur)
+        assert proof[i] == ko.mul(po.evaluate(R, q, taus[i + 1:]) if len(q) > 1 else q[0], ko.G1), (batch, i)
+        cur = ko.get_remainder(cur, point[i])
+    k.close()

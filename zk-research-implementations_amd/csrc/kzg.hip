@@ -114,30 +114,40 @@ constexpr uint64_t kMsmMinThreads = 1u << 17;
 // sums cost ~0.9-2 ns per bucket against ~0.21 ns per bucket-sum entry (round 5
 // rocprof of get_proof's MSMs): kBucketCost 5.
 constexpr double kBucketCost = 5.0;
-inline uint32_t msm_window_bits(uint64_t n, uint32_t lg) {
+// levels > 0: `levels` level-batched MSMs of 1, 2, 4, ... points (n = 2^levels - 1),
+// each with its own windows: the window sums cost levels times as much.
+inline uint32_t msm_window_bits(uint64_t n, uint32_t lg, uint32_t levels = 0) {
   if (const char* e = getenv("ZK_MSM_C")) {  // (diagnostic) a fixed width, 6..20
     const uint32_t f = (uint32_t)strtoul(e, nullptr, 0);
     if (f >= 6 && f <= 20) return f;
   }
-  if (lg < 12) return std::min<uint32_t>(20, std::max<uint32_t>(6, lg > 9 ? lg - 3 : 6));
-  uint32_t best = 16;
+  if (lg < 12 && levels == 0) return std::min<uint32_t>(20, std::max<uint32_t>(6, lg > 9 ? lg - 3 : 6));
+  uint32_t best = 0;
   double best_cost = 1e300;
-  for (uint32_t cc : {8u, 10u, 13u, 16u, 20u}) {
-    const double W = (double)((256 + cc - 1) / cc);
-    const double cost = (double)n * W + kBucketCost * W * (double)(1ull << (cc - 1));
+  for (uint32_t cc : {6u, 8u, 10u, 13u, 16u, 20u}) {
+    const uint32_t W = (256 + cc - 1) / cc, bb = (256 + W - 1) / W - 1;
+    const uint32_t Wt = levels ? levels * W : W;
+    if ((uint64_t)Wt << (bb - zk::sort_fine_bits(bb)) > zk::kSortBinsMax) continue;  // the sort's coarse bins
+    if (levels == 0 && cc == 6) continue;  // (single MSMs of 2^12+ points: 8 bits and up)
+    const double cost = (double)n * W + kBucketCost * Wt * (double)(1ull << bb);
     if (cost < best_cost) {
       best_cost = cost;
       best = cc;
     }
   }
+  if (!best) fail(ZK_EINVAL, "internal: no MSM window width fits the sort's bins");
   return best;
 }
 
-// sum_i scalars[i] * bases[i]; scalars canonical Fr (device), bases affine Montgomery (device)
-G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
+// The window sums of a c-bit signed-digit Pippenger of sum_i scalars[i] *
+// bases[i] (scalars canonical Fr, bases affine Montgomery, both on the
+// device): W windows of cb bits, or with levels > 0 the levels x W window sums
+// of `levels` level-batched MSMs (n = 2^levels - 1: level v = points
+// [2^v - 1, 2^(v+1) - 1), window v W + w) in one pass.
+std::vector<G1J> msm_window_sums(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n, uint32_t levels,
+                                 uint32_t& W_out, uint32_t& cb_out) {
   using namespace zk;
-  if (n == 0) return g1_inf();
-  require(n < (1ull << 28), "MSM too large");
+  require(n > 0 && n < (1ull << 28), "MSM too large");
   uint32_t lg = 0;
   while ((2ull << lg) <= n) ++lg;
   // c-bit signed digits (msm.hpp signed_digits): W c >= 256, 2^(c-1) buckets per window.
@@ -147,11 +157,14 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   // a sliver sends every point to a handful of buckets, whose long segments
   // take extra reduction levels) — that minimises n W + kBucketCost W 2^(c-1)
   // (bucket additions against the window sums' per-bucket cost).
-  const uint32_t c0 = msm_window_bits(n, lg);
+  const uint32_t c0 = msm_window_bits(n, lg, levels);
   const uint32_t W = (256 + c0 - 1) / c0;
   const uint32_t cb = (256 + W - 1) / W;
   const uint32_t bb = cb - 1;  // bucket key bits
-  const uint64_t nb = (uint64_t)W << bb;
+  const uint32_t Wt = levels ? levels * W : W;  // windows of the pass
+  const uint64_t nb = (uint64_t)Wt << bb;
+  W_out = W;
+  cb_out = cb;
   require((uint64_t)n * W < (1ull << 32), "MSM too large");  // u32 entry offsets
   DevBuf& cnt = c->msm[10];
   DevBuf& cur = c->msm[11];
@@ -159,7 +172,7 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   cnt.ensure((nb + 1) * 4);
   ord.ensure(std::max<uint64_t>(1, n * W) * 4);
   {  // bucket sort (msm.hpp k_sort_hist / k_sort_scatter / k_sort_fine)
-    const uint32_t C = bb - sort_fine_bits(bb), nbin = W << C;
+    const uint32_t C = bb - sort_fine_bits(bb), nbin = Wt << C;
     require(nbin <= kSortBinsMax, "internal: MSM coarse bins exceed the LDS table");
     const uint32_t pts = sort_block_pts(n);
     const uint32_t NB = (uint32_t)((n + pts - 1) / pts);
@@ -168,9 +181,9 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
     DevBuf& ent = c->msm[16];
     ent.ensure(std::max<uint64_t>(1, n * W) * 8);
     HIPCK(hipMemsetAsync(cur.p, 0, nh * 4, c->stream));
-    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist, NB, scalars, n, cb, W, NB, pts, dptr<uint32_t>(cur));
+    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist, NB, scalars, n, cb, W, levels, NB, pts, dptr<uint32_t>(cur));
     scan_u32(c, dptr<uint32_t>(cur), nh);
-    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, NB, pts,
+    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, levels, NB, pts,
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint64_t>(ent));
     launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), bb, NB,
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
@@ -212,12 +225,12 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
   }
   // per window: sum_d d B_d over chunks of buckets, then over the chunks
   uint32_t bchunk = kBucketChunkMax;  // buckets per thread: fewer when the windows are small (thread count)
-  while (bchunk > 1 && ((uint64_t)W << bb) / bchunk < kMsmMinThreads) bchunk >>= 1;
+  while (bchunk > 1 && ((uint64_t)Wt << bb) / bchunk < kMsmMinThreads) bchunk >>= 1;
   const uint32_t chunks = (1u << bb) / bchunk;
   DevBuf& chb = c->msm[13];
-  chb.ensure((size_t)W * (chunks + 1) * sizeof(G1J));
-  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)W * (chunks + 1)), (const G1J*)buckets, bb, W, bchunk,
-         dptr<G1J>(chb));
+  chb.ensure((size_t)Wt * (chunks + 1) * sizeof(G1J));
+  launch(c, ZK_K_MSM, 0, 0, k_window_chunks, blocks_for((uint64_t)Wt * (chunks + 1)), (const G1J*)buckets, bb, Wt,
+         bchunk, dptr<G1J>(chb));
   // the W window sums: equal segments of chunks + 1 points, reduced in levels
   // of msm_win_task points per thread (short tasks keep every level parallel;
   // the sizes are known here, so no scans and no host syncs)
@@ -229,23 +242,48 @@ G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
     while (len > 1) {
       const uint32_t olen = (len + task - 1) / task;
       DevBuf& ob = c->msm[5 + flip];
-      ob.ensure((size_t)W * olen * sizeof(G1J));
-      launch(c, ZK_K_MSM, 0, 0, k_sum_uniform, blocks_for((uint64_t)W * olen), ws, len, W, task, dptr<G1J>(ob));
+      ob.ensure((size_t)Wt * olen * sizeof(G1J));
+      launch(c, ZK_K_MSM, 0, 0, k_sum_uniform, blocks_for((uint64_t)Wt * olen), ws, len, Wt, task, dptr<G1J>(ob));
       ws = dptr<G1J>(ob);
       len = olen;
       flip ^= 1;
     }
   }
-  std::vector<G1J> S(W);
-  HIPCK(hipMemcpyAsync(S.data(), ws, W * sizeof(G1J), hipMemcpyDeviceToHost, c->stream));
+  std::vector<G1J> S(Wt);
+  HIPCK(hipMemcpyAsync(S.data(), ws, Wt * sizeof(G1J), hipMemcpyDeviceToHost, c->stream));
   sync(c);
-  // Horner over the windows on the host: R = sum_w 2^(c w) S_w
+  return S;
+}
+
+// Horner over W windows of cb bits on the host: sum_w 2^(cb w) S[w]
+G1J windows_horner(const G1J* S, uint32_t W, uint32_t cb) {
+  using namespace zk;
   G1J R = S[W - 1];
   for (uint32_t w = W - 1; w-- > 0;) {
     for (uint32_t k = 0; k < cb; ++k) R = g1_dbl(R);
     R = g1_add(R, S[w]);
   }
   return R;
+}
+
+// sum_i scalars[i] * bases[i]; scalars canonical Fr (device), bases affine Montgomery (device)
+G1J msm_g1_device(zk_ctx* c, const G1A* bases, const Fe* scalars, uint64_t n) {
+  if (n == 0) return zk::g1_inf();
+  uint32_t W = 0, cb = 0;
+  const std::vector<G1J> S = msm_window_sums(c, bases, scalars, n, 0, W, cb);
+  return windows_horner(S.data(), W, cb);
+}
+
+// `levels` MSMs in one pass: out[v] = sum over points [2^v - 1, 2^(v+1) - 1)
+// (level v: 2^v points) of scalars[i] * bases[i] — kzg_get_proof's small
+// quotient commitments against the setup's suffix bases, which it stores in
+// exactly this layout (zk_kzg::level)
+std::vector<G1J> msm_levels(zk_ctx* c, const G1A* bases, const Fe* scalars, uint32_t levels) {
+  uint32_t W = 0, cb = 0;
+  const std::vector<G1J> S = msm_window_sums(c, bases, scalars, ((uint64_t)1 << levels) - 1, levels, W, cb);
+  std::vector<G1J> out(levels);
+  for (uint32_t v = 0; v < levels; ++v) out[v] = windows_horner(S.data() + (size_t)v * W, W, cb);
+  return out;
 }
 
 // batch Jacobian -> affine on the host (Montgomery's trick)
@@ -433,6 +471,17 @@ void upload_fr_canonical(zk_ctx* c, zk_repr repr, const zk_fe* host, uint64_t n,
          (const Fe*)dev, dev, n);
 }
 
+// kzg_get_proof commits the quotients of its last this many levels (<= 2^14 - 1
+// points in all) in one level-batched MSM pass (ZK_PROOF_BATCH_LEVELS: fewer,
+// 0 = one MSM per level)
+constexpr uint32_t kProofBatchLevelsMax = 14;
+uint32_t proof_batch_levels() {
+  const char* e = getenv("ZK_PROOF_BATCH_LEVELS");
+  const uint32_t x = e ? (uint32_t)strtoul(e, nullptr, 0) : kProofBatchLevelsMax;
+  return std::min(x, kProofBatchLevelsMax);
+}
+#define kProofBatchLevels proof_batch_levels()
+
 G1J kzg_commit_canonical(zk_ctx* c, const zk_kzg* k, uint32_t v, const Fe* scalars) {
   return msm_g1_device(c, k->level(v), scalars, (uint64_t)1 << v);
 }
@@ -453,18 +502,32 @@ void kzg_get_proof(zk_ctx* c, const zk_kzg* k, const Fe* f_mont, const Fe& v_mon
   Fe* nxt = cur + N;
   Fe* q = nxt + N / 2;
   launch(c, ZK_K_FOLD, 64.0 * N, 0, k_sub_const<Fr381>, grid_for(c, N, k_sub_const<Fr381>), f_mont, N, v_mont, cur);
-  out.clear();
+  out.assign(nv, g1_inf());
+  // quotients of <= 2^kProofBatchLevels - 1 points (the last kProofBatchLevels
+  // levels): written at the offsets of their suffix bases and committed
+  // together in one level-batched pass (msm_levels) — each alone is a chain of
+  // latency-bound launches (1.5-2.7 ms at 2^14 points and fewer)
+  const uint32_t nbatch = std::min<uint32_t>(nv, kProofBatchLevels);
+  DevBuf& qb = c->msm[8];
+  qb.ensure((((uint64_t)1 << nbatch) - 1 + 1) * 32);
+  Fe* qall = reinterpret_cast<Fe*>(qb.p);
   for (uint32_t i = 0; i < nv; ++i) {
     const uint32_t m = nv - i;  // variables of cur
     const uint64_t half = (uint64_t)1 << (m - 1);
+    const bool batched = m - 1 < nbatch;
+    Fe* qi = batched ? qall + (half - 1) : q;
     launch(c, ZK_K_FOLD, 96.0 * half, 0, k_top_diff<Fr381>, grid_for(c, half, k_top_diff<Fr381>), (const Fe*)cur,
-           half, q);
+           half, qi);
     launch(c, ZK_K_CONVERT, 64.0 * half, (double)half, k_convert<Fr381, false>,
-           grid_for(c, half, k_convert<Fr381, false>), (const Fe*)q, q, half);
-    out.push_back(kzg_commit_canonical(c, k, m - 1, q));
+           grid_for(c, half, k_convert<Fr381, false>), (const Fe*)qi, qi, half);
+    if (!batched) out[i] = kzg_commit_canonical(c, k, m - 1, q);
     launch(c, ZK_K_FOLD, 96.0 * half, (double)half, k_fold<Fr381>, grid_for(c, half, k_fold<Fr381>), (const Fe*)cur,
            nxt, half, m - 1, point[i]);
     std::swap(cur, nxt);
+  }
+  if (nbatch) {
+    const std::vector<G1J> lv = msm_levels(c, k->level(0), qall, nbatch);
+    for (uint32_t v = 0; v < nbatch; ++v) out[nv - 1 - v] = lv[v];  // level v = quotient i = nv - 1 - v
   }
 }
 }  // namespace

@@ -120,33 +120,46 @@ __host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t 
   const uint32_t F = sort_fine_bits(b), C = b - F;
   return ((key & ((1u << C) - 1u)) << F) | (key >> C);
 }
+// Level-batched MSMs (msm_levels, kzg_get_proof's small quotients): point i
+// belongs to level floor(log2(i + 1)) — levels of 1, 2, 4, ... points laid out
+// back to back, as the setup stores its Lagrange bases — and its digits go to
+// that level's W windows: window index level W + w of Wt = levels W.
+__device__ __forceinline__ uint32_t point_window0(uint64_t i, uint32_t W, uint32_t levels) {
+  return levels ? (63u - (uint32_t)__builtin_clzll(i + 1)) * W : 0u;
+}
 __global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
-                                                      uint32_t W, uint32_t NB, uint32_t pts, uint32_t* __restrict__ H) {
+                                                      uint32_t W, uint32_t levels, uint32_t NB, uint32_t pts,
+                                                      uint32_t* __restrict__ H) {
   __shared__ uint32_t hist[kSortBinsMax];
-  const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = W << C;
+  const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = (levels ? levels * W : W) << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) hist[j] = 0;
   __syncthreads();
   const uint64_t p0 = (uint64_t)blockIdx.x * pts, p1 = p0 + pts < n ? p0 + pts : n;
-  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
-    signed_digits(ld_fe(scalars, i), c, W,
-                  [&](uint32_t w, uint32_t key, uint32_t) { atomicAdd(&hist[(w << C) + (key & ((1u << C) - 1u))], 1u); });
+  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
+    const uint32_t w0 = point_window0(i, W, levels);
+    signed_digits(ld_fe(scalars, i), c, W, [&](uint32_t w, uint32_t key, uint32_t) {
+      atomicAdd(&hist[((w0 + w) << C) + (key & ((1u << C) - 1u))], 1u);
+    });
+  }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) H[(uint64_t)j * NB + blockIdx.x] = hist[j];
 }
 __global__ __launch_bounds__(kBlock) void k_sort_scatter(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
-                                                         uint32_t W, uint32_t NB, uint32_t pts,
+                                                         uint32_t W, uint32_t levels, uint32_t NB, uint32_t pts,
                                                          const uint32_t* __restrict__ Hs, uint64_t* __restrict__ E) {
   __shared__ uint32_t cur[kSortBinsMax];
-  const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = W << C;
+  const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = (levels ? levels * W : W) << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) cur[j] = Hs[(uint64_t)j * NB + blockIdx.x];
   __syncthreads();
   const uint64_t p0 = (uint64_t)blockIdx.x * pts, p1 = p0 + pts < n ? p0 + pts : n;
-  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock)
+  for (uint64_t i = p0 + threadIdx.x; i < p1; i += kBlock) {
+    const uint32_t w0 = point_window0(i, W, levels);
     signed_digits(ld_fe(scalars, i), c, W, [&](uint32_t w, uint32_t key, uint32_t neg) {
-      const uint32_t pos = atomicAdd(&cur[(w << C) + (key & ((1u << C) - 1u))], 1u);
+      const uint32_t pos = atomicAdd(&cur[((w0 + w) << C) + (key & ((1u << C) - 1u))], 1u);
       ZK_DCHECK((uint64_t)pos < n * W);
       E[pos] = (i << (F + 1)) | ((uint64_t)neg << F) | (key >> C);
     });
+  }
 }
 // grid = W 2^C blocks, one per coarse bin; cnt gets (W << b) + 1 offsets (b: bucket bits)
 __global__ __launch_bounds__(kBlock) void k_sort_fine(const uint64_t* __restrict__ E, uint32_t b, uint32_t NB,
