@@ -298,13 +298,14 @@ def test_get_proof_large_window_verifies(ctx):
     k.close()
 
 
-@pytest.mark.parametrize("batch", ["0", "1", "6", "14"])
+@pytest.mark.parametrize("batch", ["0", "1", "6", "14", "20"])
 def test_get_proof_level_batched_quotients(ctx, monkeypatch, batch):
-    """kzg_get_proof commits its last ZK_PROOF_BATCH_LEVELS quotients (14 by
-    default: <= 2^13 points each) in one level-batched MSM pass (msm_levels:
+    """kzg_get_proof commits its last ZK_PROOF_BATCH_LEVELS quotients (20 by
+    default: <= 2^19 points each) in one level-batched MSM pass (msm_levels:
     level v = points [2^v - 1, 2^(v+1) - 1) of the suffix bases, its own W
     windows); every split gives the per-level proof, and each element equals
-    q_i(taus) * G1 (16 variables: two levels committed alone at 14)."""
+    q_i(taus) * G1 (16 variables: two levels committed alone at 14, all
+    batched at 20)."""
     rng = random.Random(31)
     n = 16
     taus = [rng.randrange(R) for _ in range(n)]

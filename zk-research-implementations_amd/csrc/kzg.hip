@@ -471,10 +471,10 @@ void upload_fr_canonical(zk_ctx* c, zk_repr repr, const zk_fe* host, uint64_t n,
          (const Fe*)dev, dev, n);
 }
 
-// kzg_get_proof commits the quotients of its last this many levels (<= 2^14 - 1
+// kzg_get_proof commits the quotients of its last this many levels (<= 2^20 - 1
 // points in all) in one level-batched MSM pass (ZK_PROOF_BATCH_LEVELS: fewer,
 // 0 = one MSM per level)
-constexpr uint32_t kProofBatchLevelsMax = 14;
+constexpr uint32_t kProofBatchLevelsMax = 20;
 uint32_t proof_batch_levels() {
   const char* e = getenv("ZK_PROOF_BATCH_LEVELS");
   const uint32_t x = e ? (uint32_t)strtoul(e, nullptr, 0) : kProofBatchLevelsMax;
@@ -503,9 +503,9 @@ void kzg_get_proof(zk_ctx* c, const zk_kzg* k, const Fe* f_mont, const Fe& v_mon
   Fe* q = nxt + N / 2;
   launch(c, ZK_K_FOLD, 64.0 * N, 0, k_sub_const<Fr381>, grid_for(c, N, k_sub_const<Fr381>), f_mont, N, v_mont, cur);
   out.assign(nv, g1_inf());
-  // quotients of <= 2^kProofBatchLevels - 1 points (the last kProofBatchLevels
-  // levels): written at the offsets of their suffix bases and committed
-  // together in one level-batched pass (msm_levels) — each alone is a chain of
+  // the quotients of the last kProofBatchLevels levels (<= 2^19 points each):
+  // written at the offsets of their suffix bases and committed together in one
+  // level-batched pass (msm_levels) — alone, each small one is a chain of
   // latency-bound launches (1.5-2.7 ms at 2^14 points and fewer)
   const uint32_t nbatch = std::min<uint32_t>(nv, kProofBatchLevels);
   DevBuf& qb = c->msm[8];

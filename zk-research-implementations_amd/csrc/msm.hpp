@@ -114,7 +114,7 @@ __host__ __device__ __forceinline__ uint32_t sort_block_pts(uint64_t n) {
   const uint64_t p = (n + 255) / 256;
   return (uint32_t)(p < 1024 ? 1024 : (p > kSortPts ? kSortPts : p));
 }
-constexpr uint32_t kSortBinsMax = 13312;    // W 2^C over c = 6..20 (c = 20: 13 x 1024)
+constexpr uint32_t kSortBinsMax = 16896;    // Wt 2^C: c = 20: 13 x 1024; 20 batched levels of 10 bits: 520 x 32
 __host__ __device__ __forceinline__ uint32_t sort_fine_bits(uint32_t b) { return b / 2; }
 __host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t b) {
   const uint32_t F = sort_fine_bits(b), C = b - F;
