@@ -3,7 +3,9 @@ tests/test_gpu_sharded.py; not a test module itself).
 
 env: RANK, WORLD_SIZE, MASTER_PORT, COMM in {host, rccl, none}, FIELD, NLOCAL, OUT
 (+ optional SEED, default 19; PEER=1: zk_ctx_attach_peer_reduce after the
-communicator, so the steps' sums meet in the ranks' IPC-mapped buffers)
+communicator, so the steps' sums meet in the ranks' IPC-mapped buffers;
+PEER_MAY_FAIL=1: a refused attach is recorded, and the proof runs on the
+communicator)
 Rank g proves its low-index-bit shard; rank 0 writes the proof as JSON.
 """
 from __future__ import annotations
@@ -35,8 +37,14 @@ def main() -> None:
         ctx.attach_host_comm(rank, world, TorchAllreduce())
     elif comm == "rccl":
         rendezvous_rccl(ctx, rank, world)
+    peer_refused = None
     if os.environ.get("PEER") == "1":
-        ctx.attach_peer_reduce()
+        try:
+            ctx.attach_peer_reduce()
+        except zk_amd.ZkError as e:  # (PEER_MAY_FAIL=1: the test checks every rank refused)
+            if os.environ.get("PEER_MAY_FAIL") != "1":
+                raise
+            peer_refused = str(e)
         ctx.reset_stats()  # (the handle exchange went through the communicator)
     i0, stride = shard_layout(rank, world)
     seed = int(os.environ.get("SEED", "19"))
@@ -59,7 +67,7 @@ def main() -> None:
     res = {"polys": [[hex(x) for x in p] for p in polys],
            "chal": [hex(x) for x in to_ints(ch[:n])], "collectives": ctx.stats()["collectives"],
            "blob_keccak": zk_amd.keccak256(blob).hex(), "blob_keccak_claimed": zk_amd.keccak256(blob_c).hex(),
-           "comm": ctx.comm_info(), "peer": ctx.peer_reduce}
+           "comm": ctx.comm_info(), "peer": ctx.peer_reduce, "peer_refused": peer_refused}
     with open(os.path.join(os.environ["OUT"], f"rank{rank}.json"), "w") as fh:
         json.dump(res, fh)
     dist.barrier()

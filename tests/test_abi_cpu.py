@@ -133,7 +133,7 @@ def test_reference_shaped_constructors_panic_like_reference():
         zk_amd.MultilinearPoly([1, 2, 3])
     with pytest.raises(ValueError):
         zk_amd.MultilinearPoly([])
-    with pytest.raises(ValueError):  # composed_polynomial.rs:357-374
+    with pytest.raises(ValueError):  # ProductPoly::new's length check (composed_polynomial.rs:19-21), the panic test :157-175
         zk_amd.ProductPoly([[0, 0, 0, 3], [0, 0, 0, 4, 0, 0, 0, 4]])
     pp = zk_amd.ProductPoly([[0, 0, 0, 3]])
     with pytest.raises(ValueError):

@@ -222,3 +222,33 @@ def test_circuit_with_input_kzg_at_scale(ctx):
     kp = got.input_proof
     bad = dataclasses.replace(kp, opened_evals=(kp.opened_evals[0], (kp.opened_evals[1] + 1) % p))
     assert not verify(dataclasses.replace(got, input_proof=bad), circ)
+
+
+def test_default_entropy_taus_like_the_reference(ctx):
+    """gkr::prove's default matches the reference's shape (gkr_protocol.rs:92-118):
+    a BLS12-381 Fr circuit always gets the input layer's KZG step, over taus
+    drawn from entropy (os.urandom here, StdRng::from_entropy there), so two
+    proofs of the same circuit carry different setups and commitments but the
+    same layer sum-checks, and both verify (without the inputs, and with them);
+    taus=None skips the step; a BN254 circuit (whose reference gkr::prove cannot
+    build the BLS12-381 KZG) gets no input proof."""
+    import dataclasses
+
+    structure = [[A, A, A, A], [M, A], [A]]
+    inputs = [5, 2, 2, 4, 10, 0, 3, 3]
+    circ = Circuit([[OPS[o] for o in layer] for layer in structure], 2)
+    a, b = prove(circ, inputs, ctx), prove(circ, inputs, ctx, taus="entropy")
+    for pr in (a, b):
+        assert pr.input_proof is not None and len(pr.input_proof.g2_taus) == 3
+        assert verify(pr, circ) and verify(pr, circ, inputs)
+        assert not verify(pr, circ, [5, 2, 2, 4, 10, 0, 3, 4])  # inputs given: checked against the openings
+    assert a.input_proof.g2_taus != b.input_proof.g2_taus and a.input_proof.commitment != b.input_proof.commitment
+    assert a.proof_polynomials == b.proof_polynomials and a.input_evaluations == b.input_evaluations
+    bad = dataclasses.replace(a.input_proof, proof=(b.input_proof.proof[0], a.input_proof.proof[1]))
+    assert not verify(dataclasses.replace(a, input_proof=bad), circ)  # an opening under another setup
+    c = prove(circ, inputs, ctx, taus=None)
+    assert c.input_proof is None and c.proof_polynomials == a.proof_polynomials and verify(c, circ, inputs)
+    bn = prove(Circuit([[OPS[o] for o in layer] for layer in structure], 0), inputs, ctx)
+    assert bn.input_proof is None and verify(bn, Circuit([[OPS[o] for o in layer] for layer in structure], 0), inputs)
+    with pytest.raises(ValueError):
+        prove(circ, inputs, ctx, taus="urandom")

@@ -278,11 +278,17 @@ def test_bucket_sum_paths_agree(monkeypatch, balanced):
         ctx.close()
 
 
-def test_get_proof_large_window_verifies(ctx):
-    """KZG::get_proof (kzg.rs:59-95) at 20 variables — quotient MSMs of 2^19
-    .. 1 points, the large signed windows (c up to 16) and the balanced bucket
-    sums — accepted by KZG::verify's pairings (kzg.rs:97-129) and rejected with
-    a wrong opened value or a swapped proof."""
+@pytest.mark.parametrize("batch", ["0", None])
+def test_get_proof_large_window_verifies(ctx, monkeypatch, batch):
+    """KZG::get_proof (kzg.rs:59-95) at 20 variables, accepted by KZG::verify's
+    pairings (kzg.rs:97-129) and rejected with a wrong opened value or a
+    swapped proof. ZK_PROOF_BATCH_LEVELS=0: every quotient is its own MSM (2^19
+    .. 1 points: the large signed windows, c up to 16, and the balanced bucket
+    sums — the per-level path that otherwise runs only for levels of 2^20 points
+    and more); default: all 20 levels in the one level-batched pass
+    (msm_levels). (the per-level large-window path stays covered.)"""
+    if batch is not None:
+        monkeypatch.setenv("ZK_PROOF_BATCH_LEVELS", batch)
     rng = random.Random(20)
     n = 20
     taus = [rng.randrange(R) for _ in range(n)]

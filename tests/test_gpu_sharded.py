@@ -205,3 +205,21 @@ def test_peer_reduce_config4_workload_8_ranks(tmp_path):
         assert r["peer"] is True
         assert r["chal"] == [hex(int(c, 16)) for c in fix["challenges"]], f"rank {rank}"
         assert r["blob_keccak_claimed"] == fix["blob_keccak256"], f"rank {rank}"
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 1), (4, 0)])
+def test_peer_attach_refused_on_every_rank_when_one_check_fails(tmp_path, world, fail_rank):
+    """the attach-time check's outcome is agreed over the world. One
+    rank's check is made to fail (ZK_PEER_CHECK_FAIL_RANK): EVERY rank's
+    zk_ctx_attach_peer_reduce must then refuse (ZK_ECOMM), no rank may keep
+    peer mode, and the proof that follows on the communicator must still be
+    the oracle's on every rank (no rank waits in a peer kernel or the
+    communicator for one that dropped out)."""
+    res = _run(world, "host", 0, 12, str(tmp_path), {"PEER": "1", "PEER_MAY_FAIL": "1",
+                                                    "ZK_PEER_CHECK_FAIL_RANK": str(fail_rank)})
+    want = _oracle(0, 12 + world.bit_length() - 1)
+    for rank, r in enumerate(res):
+        assert r["peer"] is False and r["peer_refused"], f"rank {rank}"
+        assert ("another rank" in r["peer_refused"]) == (rank != fail_rank), r["peer_refused"]
+        assert {"polys": r["polys"], "chal": r["chal"], "blob_keccak": r["blob_keccak"]} == want, f"rank {rank}"
+        assert r["collectives"] == _collectives(12)

@@ -1,0 +1,144 @@
+// Round 6: memory-only variants of the first k_gkr_t33's access pattern (the
+// W8 shape of microbench_wmix.hip: per chunk of 64 octants a wave folds eight
+// corners, each fold reading eight 2 KiB runs — inputs e + k 8 O, k < 8 — and
+// writing one 2 KiB run at e = ch 64 + l + f O; xor instead of arithmetic) with
+// what the kernel could still change without a new layout:
+//   STRIDE  chunks ch = b, b + G, ... (the kernel's order: all blocks on adjacent chunks)
+//   BLOCK   block b takes chunks [b cpb, (b + 1) cpb) (each block walks its own region)
+//   ROT     STRIDE, but block b starts its eight folds at corner b % 8 (concurrent
+//           writes spread over eight regions instead of one)
+// each with one or two folds of loads in flight (AHEAD; the kernel runs two).
+// Sizes: 4 input tables of 2^24 x 32 B (2.15 GB read), 4 outputs of 2^21 x 32 B.
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/mb_order tools/microbench_order.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+enum { STRIDE = 0, BLOCK = 1, ROT = 2 };
+struct Tabs {
+  const uint4* in[4];
+  uint4* out[4];
+};
+__device__ __forceinline__ void xr(uint4& a, const uint4& c) {
+  a.x ^= c.x;
+  a.y ^= c.y;
+  a.z ^= c.z;
+  a.w ^= c.w;
+}
+
+// O: octants of the output level; the 8 inputs of output e are e + k 8 O
+template <int ORDER, int AHEAD, bool ST>
+__global__ __launch_bounds__(256, 1) void k_order(Tabs t, size_t O) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* __restrict__ X = t.in[w];
+  uint4* __restrict__ X2 = t.out[w];
+  const size_t nch = O / 64, h8 = 8 * O;
+  const size_t G = gridDim.x, cpb = nch / G;  // (host: nch % G == 0)
+  const int f0 = ORDER == ROT ? (int)(blockIdx.x & 7) : 0;
+  auto chunk = [&](size_t i) -> size_t { return ORDER == BLOCK ? blockIdx.x * cpb + i : blockIdx.x + i * G; };
+  // unit u = i 8 + f: fold f of the block's i-th chunk; loads of unit u into slot u % (AHEAD + 1)
+  constexpr int NS = AHEAD + 1;
+  uint4 a[NS][8], b[NS][8];
+  const size_t units = cpb * 8;
+  auto load = [&](size_t u, int s) {
+    const size_t uu = u < units ? u : 0;  // (past the end: unit 0 again, unconditional like the kernel)
+    const size_t e = chunk(uu / 8) * 64 + l + (size_t)((f0 + uu % 8) & 7) * O;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a[s][k] = X[2 * (e + k * h8)];
+      b[s][k] = X[2 * (e + k * h8) + 1];
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < AHEAD; ++s) load(s, s);
+  for (size_t u0 = 0; u0 < units; u0 += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const size_t u = u0 + s;
+      load(u + AHEAD, (s + AHEAD) % NS);
+      if (u < units) {
+        uint4 x = a[s][0], y = b[s][0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+          xr(x, a[s][k]);
+          xr(y, b[s][k]);
+        }
+        const size_t e = chunk(u / 8) * 64 + l + (size_t)((f0 + u % 8) & 7) * O;
+        if (ST) {
+          X2[2 * e] = x;
+          X2[2 * e + 1] = y;
+        } else if ((x.x ^ y.y) == 0x12345678u) {
+          X2[2 * e] = x;
+        }
+      }
+    }
+  }
+}
+
+template <int ORDER, int AHEAD, bool ST>
+float run(const Tabs& t, size_t O, int grid, int reps) {
+  const size_t nch = O / 64;
+  if (O % 64 || nch % grid || 8 * O * 8 > (1ull << 24)) {
+    fprintf(stderr, "bad sizes\n");
+    exit(1);
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> v;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_order<ORDER, AHEAD, ST>), dim3(grid), dim3(256), 0, 0, t, O);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    v.push_back(ms * 1000.f);
+  }
+  std::sort(v.begin(), v.end());
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return v[v.size() / 2];
+}
+
+int main() {
+  const size_t N = 1ull << 24;
+  Tabs t;
+  for (int i = 0; i < 4; ++i) {
+    uint4* p;
+    CK(hipMalloc(&p, N * 32));
+    CK(hipMemset(p, 0x11 * (i + 1), N * 32));
+    t.in[i] = p;
+    CK(hipMalloc(&t.out[i], N / 8 * 32));
+  }
+  const size_t O = N / 64;  // 2^18 octants
+  const double rd = 4.0 * N * 32, wr = 4.0 * N / 8 * 32;
+  const int reps = 9;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int grid : {256, 512}) {
+      const float s1 = run<STRIDE, 1, true>(t, O, grid, reps), s2 = run<STRIDE, 2, true>(t, O, grid, reps);
+      const float b1 = run<BLOCK, 1, true>(t, O, grid, reps), b2 = run<BLOCK, 2, true>(t, O, grid, reps);
+      const float r1 = run<ROT, 1, true>(t, O, grid, reps), r2 = run<ROT, 2, true>(t, O, grid, reps);
+      const float s2r = run<STRIDE, 2, false>(t, O, grid, reps), b2r = run<BLOCK, 2, false>(t, O, grid, reps);
+      auto tb = [&](float us, double by) { return by / us / 1e6; };
+      printf("grid %d W8: stride %6.1f us (%.2f TB/s) / 2 ahead %6.1f (%.2f) | blocked %6.1f (%.2f) / %6.1f (%.2f) | "
+             "rotated corners %6.1f (%.2f) / %6.1f (%.2f) || R8 2 ahead: stride %6.1f (%.2f) blocked %6.1f (%.2f)\n",
+             grid, s1, tb(s1, rd + wr), s2, tb(s2, rd + wr), b1, tb(b1, rd + wr), b2, tb(b2, rd + wr), r1, tb(r1, rd + wr),
+             r2, tb(r2, rd + wr), s2r, tb(s2r, rd), b2r, tb(b2r, rd));
+      fflush(stdout);
+    }
+  }
+  return 0;
+}

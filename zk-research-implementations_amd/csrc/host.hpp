@@ -250,6 +250,10 @@ struct zk_ctx {
   std::vector<void*> peer_open;       // the peers' buffers, opened from their IPC handles
   zk::PeerSlots* d_peer = nullptr;    // device copy of the slot table
   uint64_t peer_seq = 0;              // last reduction's sequence tag (the same on every rank)
+  // RCCL steps: the publish of the last all-reduce not yet enqueued (host.hpp
+  // take_publish / flush_publish), and whether the next step may take it
+  bool pub_pending = false, defer_publish = false;
+  uint32_t pub_n = 0, pub_tag = 0;
   // KZG / MSM scratch (grow-only) and the cached fixed-base table of G1
   DevBuf msm[19];
   bool msm_balanced = true;  // ZK_MSM_BALANCED: bucket sums in equal tasks across bucket boundaries (kzg.hip)
@@ -514,24 +518,41 @@ inline void launch_peer_gather(zk_ctx* c, const void* src, uint64_t n) {
 inline size_t peer_gather_bytes(int world) {
   return ((size_t)world * 4 * ((size_t)1 << zk::kPeerGatherMaxT) * 4 + zk::kPeerMax) * sizeof(uint64_t);
 }
+// One attach phase's outcome agreed over the world: true only if
+// every rank passed. Every rank calls it at the same points of peer_attach,
+// whatever its own outcome, so no rank keeps peer mode (or waits in a peer
+// kernel, or in the communicator) while another has dropped out.
+inline bool peer_consensus(zk_ctx* c, bool ok) {
+  uint64_t bad = ok ? 0 : 1;
+  allreduce_host(c, &bad, 1);
+  return bad == 0;
+}
 inline void peer_attach(zk_ctx* c) {
   const size_t bytes = 2 * (size_t)c->world * zk::kPeerSlotU64 * sizeof(uint64_t), gbytes = peer_gather_bytes(c->world);
-  HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_buf), bytes, hipDeviceMallocUncached));
-  HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_gbuf), gbytes, hipDeviceMallocUncached));
-  HIPCK(hipMemset(c->peer_buf, 0, bytes));
-  HIPCK(hipMemset(c->peer_gbuf, 0, gbytes));
-  HIPCK(hipDeviceSynchronize());
-  hipIpcMemHandle_t h[2];
-  HIPCK(hipIpcGetMemHandle(&h[0], c->peer_buf));
-  HIPCK(hipIpcGetMemHandle(&h[1], c->peer_gbuf));
   constexpr size_t HW = (2 * sizeof(hipIpcMemHandle_t) + 7) / 8;
   std::vector<uint64_t> w(HW * c->world, 0);
-  memcpy(&w[HW * c->rank], h, sizeof h);
+  std::string why;
+  // phase 1: our buffers and their handles (a rank that fails here still takes
+  // part in the exchange, with zero handles, and in the consensus below)
+  try {
+    HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_buf), bytes, hipDeviceMallocUncached));
+    HIPCK(hipExtMallocWithFlags(reinterpret_cast<void**>(&c->peer_gbuf), gbytes, hipDeviceMallocUncached));
+    HIPCK(hipMemset(c->peer_buf, 0, bytes));
+    HIPCK(hipMemset(c->peer_gbuf, 0, gbytes));
+    HIPCK(hipDeviceSynchronize());
+    hipIpcMemHandle_t h[2];
+    HIPCK(hipIpcGetMemHandle(&h[0], c->peer_buf));
+    HIPCK(hipIpcGetMemHandle(&h[1], c->peer_gbuf));
+    memcpy(&w[HW * c->rank], h, sizeof h);
+  } catch (const ZkError& e) {
+    why = e.msg;
+  }
   allreduce_host(c, w.data(), w.size());  // disjoint slots: the sum is the gather
   zk::PeerSlots ps{};
   ps.world = (uint32_t)c->world;
   ps.rank = (uint32_t)c->rank;
-  for (int r = 0; r < c->world; ++r) {
+  // phase 2: the peers' buffers
+  for (int r = 0; r < c->world && why.empty(); ++r) {
     if (r == c->rank) {
       ps.slot[r] = c->peer_buf;
       ps.gather[r] = c->peer_gbuf;
@@ -539,22 +560,30 @@ inline void peer_attach(zk_ctx* c) {
     }
     hipIpcMemHandle_t hr[2];
     memcpy(hr, &w[HW * r], sizeof hr);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 2 && why.empty(); ++b) {
       void* p = nullptr;
       const hipError_t e = hipIpcOpenMemHandle(&p, hr[b], hipIpcMemLazyEnablePeerAccess);
       if (e != hipSuccess) {
-        peer_release(c);
-        fail(ZK_ECOMM, std::string("peer reduction: opening rank ") + std::to_string(r) + "'s buffer: " + hipGetErrorString(e));
+        (void)hipGetLastError();
+        why = std::string("peer reduction: opening rank ") + std::to_string(r) + "'s buffer: " + hipGetErrorString(e);
+        break;
       }
       c->peer_open.push_back(p);
       (b == 0 ? ps.slot[r] : ps.gather[r]) = reinterpret_cast<uint64_t*>(p);
     }
   }
-  HIPCK(hipMalloc(reinterpret_cast<void**>(&c->d_peer), sizeof ps));
-  HIPCK(hipMemcpy(c->d_peer, &ps, sizeof ps, hipMemcpyHostToDevice));
+  if (why.empty() && (hipMalloc(reinterpret_cast<void**>(&c->d_peer), sizeof ps) != hipSuccess ||
+                      hipMemcpy(c->d_peer, &ps, sizeof ps, hipMemcpyHostToDevice) != hipSuccess)) {
+    (void)hipGetLastError();
+    why = "peer reduction: device slot table";
+  }
+  if (!peer_consensus(c, why.empty())) {
+    peer_release(c);
+    fail(ZK_ECOMM, why.empty() ? "peer reduction: another rank could not set up its buffers" : why);
+  }
   c->peer = true;
   c->peer_seq = 0;
-  // the check: the same publish path, a reduction every rank takes part in
+  // phase 3, the check: the same publish path, a reduction every rank takes part in
   zk::RoundSink sk{};
   sk.host_out = c->h_red;
   sk.host_flag = h_flag(c);
@@ -564,16 +593,20 @@ inline void peer_attach(zk_ctx* c) {
   sk.err = h_err(c);
   __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
   k_peer_check<<<1, zk::kBlock, 0, c->stream>>>(sk);
-  HIPCK(hipGetLastError());
-  HIPCK(hipStreamSynchronize(c->stream));
+  bool ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
   const uint32_t err = __atomic_load_n(h_err(c), __ATOMIC_ACQUIRE);
-  bool ok = err == 0 && __atomic_load_n(h_flag(c), __ATOMIC_ACQUIRE) == sk.tag;
+  ok = ok && err == 0 && __atomic_load_n(h_flag(c), __ATOMIC_ACQUIRE) == sk.tag;
   const uint64_t tri = (uint64_t)c->world * (c->world + 1) / 2;
   for (uint64_t t = 0; t < 16 && ok; ++t) ok = __atomic_load_n(c->h_red + t, __ATOMIC_RELAXED) == tri * (t + 1);
-  if (!ok) {
+  // (tests: ZK_PEER_CHECK_FAIL_RANK=r makes rank r report a failed check, so
+  // the world's consensus path runs: every rank must drop peer mode)
+  if (const char* fr = getenv("ZK_PEER_CHECK_FAIL_RANK"))
+    if (atoi(fr) == c->rank) ok = false;
+  if (!peer_consensus(c, ok)) {
     __atomic_store_n(h_err(c), 0u, __ATOMIC_RELAXED);
     peer_release(c);
-    fail(ZK_ECOMM, err ? "peer reduction check: a peer never arrived" : "peer reduction check: wrong sums");
+    fail(ZK_ECOMM, ok ? "peer reduction check: failed on another rank"
+                      : (err ? "peer reduction check: a peer never arrived" : "peer reduction check: wrong sums"));
   }
 }
 
@@ -625,15 +658,38 @@ inline void wait_flag(zk_ctx* c, uint32_t tag) {
 // product sums, L = 8: element sums), summed over ranks when sharded.
 // Stream side of a round's hand-off, enqueued right after its kernel: across
 // ranks over RCCL the device totals are all-reduced and then published.
+// With pre-enqueued steps (defer_publish) the publish of the all-reduced sums
+// is left to the next step kernel's block 0 (DIn::pub_*, kernels.hpp
+// wave_publish): take_publish hands it over, flush_publish launches k_publish
+// for a publish no kernel took (the phase's last step, or a next step without
+// a DIn). One kernel and one boundary fewer per sharded step.
+inline void flush_publish(zk_ctx* c) {
+  if (!c->pub_pending) return;
+  c->pub_pending = false;
+  zk::k_publish<<<1, 256, 0, c->stream>>>(d_red(c), (int)c->pub_n, c->h_red, h_flag(c), c->pub_tag);
+  HIPCK(hipGetLastError());
+}
+inline void take_publish(zk_ctx* c, zk::DIn& din) {
+  if (!c->pub_pending) return;
+  c->pub_pending = false;
+  din.pub_src = d_red(c);
+  din.pub_dst = c->h_red;
+  din.pub_flag = h_flag(c);
+  din.pub_n = c->pub_n;
+  din.pub_tag = c->pub_tag;
+}
 inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
   if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL && !c->peer) {
+    flush_publish(c);  // (d_red is about to be overwritten)
     {
       CollTimer ct(c, 8.0 * n);
       NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
     }
     c->stats.collectives += 1;
-    zk::k_publish<<<1, 256, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
-    HIPCK(hipGetLastError());
+    c->pub_pending = true;
+    c->pub_n = (uint32_t)n;
+    c->pub_tag = sk.tag;
+    if (!c->defer_publish) flush_publish(c);
   }
 }
 
@@ -1064,6 +1120,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.relay = d_rpost(c);
         din.err = h_err(c);
         din.tag = rtags[si] = ++c->rtag;
+        take_publish(c, din);
       } else {
         din.ra = rz;
         din.rb = ra;
@@ -1174,6 +1231,7 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.relay = d_rpost(c);
         din.err = h_err(c);
         din.tag = rtags[si] = ++c->rtag;
+        take_publish(c, din);
       } else if (st.np == 2) {
         din.ra = ra;
         din.rb = rb;
@@ -1235,10 +1293,19 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   PostR post{c};
   if (pre) {
     const auto t0 = std::chrono::steady_clock::now();
+    struct DeferGuard {  // (an exception mid-enqueue leaves nothing deferred for the next call)
+      zk_ctx* c;
+      ~DeferGuard() { c->defer_publish = false; c->pub_pending = false; }
+    } dg{c};
+    c->defer_publish = true;  // (a step's publish rides on the next step kernel, take_publish)
     for (size_t si = 0; si < ns; ++si) {
+      const int k = steps[si].kind;
+      if (k != GS_T33 && k != GS_T32 && k != GS_DOUBLE) flush_publish(c);  // (kernels without a DIn)
       enqueue(si);
       post.last = last_tag(si);  // from here on the guard releases what is enqueued
     }
+    c->defer_publish = false;
+    flush_publish(c);
     if (getenv("ZK_DEBUG_ENQUEUE"))
       fprintf(stderr, "zk: enqueued %zu steps (%u rounds) in %.1f us\n", ns, nv,
               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());

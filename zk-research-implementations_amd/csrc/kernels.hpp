@@ -244,6 +244,31 @@ struct PeerSlots {
   uint64_t* gather[kPeerMax];  // rank r's gather buffer: [world][4 x 2^kPeerGatherMaxT elements], then world tags
   uint32_t world, rank;
 };
+// Ordering of a peer hand-off (data words -> tag) in the memory model's own
+// terms: the producer drains its data stores, then a SYSTEM-scope
+// release fence, then the relaxed tag store; the consumer polls the tag with
+// relaxed loads, then a SYSTEM-scope acquire fence, then reads the data. The
+// buffers are uncached device memory and every data access is a system-scope
+// (sc0 sc1) access as well, so the hardware would order them without the
+// fences; ZK_PEER_FENCE=0 builds that form for the A/B of their cost
+// (profiles/r6_peer_fence_ab.txt).
+#ifndef ZK_PEER_FENCE
+#define ZK_PEER_FENCE 1
+#endif
+__device__ __forceinline__ void peer_release_fence() {
+#if ZK_PEER_FENCE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the guide's compiler hazard: the flag never overtakes the write-back)
+#endif
+}
+__device__ __forceinline__ void peer_acquire_fence() {
+#if ZK_PEER_FENCE
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the polls
+#endif
+}
 
 
 struct RoundSink {
@@ -419,9 +444,11 @@ __device__ __forceinline__ uint64_t peer_allreduce(uint64_t v, const RoundSink& 
     for (uint32_t r = 0; r < W; ++r) __hip_atomic_store(ps->slot[r] + mine + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (C > 64) __syncthreads();  // every storing wave has drained before the tags
-  if (t == 0)
+  if (t == 0) {
+    peer_release_fence();
     for (uint32_t r = 0; r < W; ++r)
       __hip_atomic_store(ps->slot[r] + mine + kPeerSlotU64 - 1, sk.peer_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   uint64_t* own = ps->slot[me];
   if (t < W) {  // lane r waits for rank r's tag
     const uint64_t* tag = own + (par * W + t) * kPeerSlotU64 + kPeerSlotU64 - 1;
@@ -435,7 +462,7 @@ __device__ __forceinline__ uint64_t peer_allreduce(uint64_t v, const RoundSink& 
     }
   }
   if (C > 64) __syncthreads();  // (C <= 64: wave 0 alone, reconverged after the polls)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the polls
+  peer_acquire_fence();  // every loading wave: after the polls (and the barrier), before the data loads
   uint64_t s = 0;
   if (t < (uint32_t)C)
     for (uint32_t r = 0; r < W; ++r) s += __hip_atomic_load(own + (par * W + r) * kPeerSlotU64 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -937,7 +964,24 @@ struct DIn {
   RPost* relay;        // device relay slot (used when gridDim > 1)
   uint32_t* err;       // pinned error word
   uint32_t tag;
+  // the previous step's publish, when it was all-reduced over RCCL on the
+  // stream right before this pre-enqueued kernel (host.hpp enqueue_reduce):
+  // block 0's wave 0 copies pub_n u64 from pub_src (device) to pub_dst (pinned)
+  // and raises *pub_flag = pub_tag before it polls for its own challenges — the
+  // k_publish kernel (and its boundary) of the non-deferred form, folded in
+  const uint64_t* pub_src;
+  uint64_t* pub_dst;
+  uint32_t* pub_flag;
+  uint32_t pub_n, pub_tag;
 };
+// wave 0 (all 64 lanes): the deferred publish of DIn (pub_src != null)
+__device__ __forceinline__ void wave_publish(const DIn& in) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t i = lane; i < in.pub_n; i += 64)
+    __hip_atomic_store(in.pub_dst + i, in.pub_src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's stores drained before the flag (one wave: in order)
+  if (lane == 0) __hip_atomic_store(in.pub_flag, in.pub_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // NV tagged values (8 words each) into s_w[8 NV] (LDS; valid after the barrier).
 // Block 0 polls the host slot and copies the words to the device relay when
 // `relay`; the other blocks poll the relay. dev_only: every block polls the
@@ -949,6 +993,7 @@ __device__ __forceinline__ void block_get_words(const DIn& in, uint32_t* s_w, bo
     const bool mine = lane < 8 * NV;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const bool direct = blockIdx.x == 0 && !dev_only;
+    if (direct && in.pub_src) wave_publish(in);
     uint64_t v = 0;
     bool ok = true;
     while (true) {

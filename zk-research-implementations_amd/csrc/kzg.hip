@@ -181,10 +181,20 @@ std::vector<G1J> msm_window_sums(zk_ctx* c, const G1A* bases, const Fe* scalars,
     DevBuf& ent = c->msm[16];
     ent.ensure(std::max<uint64_t>(1, n * W) * 8);
     HIPCK(hipMemsetAsync(cur.p, 0, nh * 4, c->stream));
-    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist, NB, scalars, n, cb, W, levels, NB, pts, dptr<uint32_t>(cur));
+    const bool big = nbin > kSortBinsSingle;  // (the level-batched pass's larger LDS table)
+    if (big)
+      launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist<kSortBinsMax>, NB, scalars, n, cb, W, levels, NB, pts,
+             dptr<uint32_t>(cur));
+    else
+      launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_hist<kSortBinsSingle>, NB, scalars, n, cb, W, levels, NB, pts,
+             dptr<uint32_t>(cur));
     scan_u32(c, dptr<uint32_t>(cur), nh);
-    launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter, NB, scalars, n, cb, W, levels, NB, pts,
-           (const uint32_t*)dptr<uint32_t>(cur), dptr<uint64_t>(ent));
+    if (big)
+      launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter<kSortBinsMax>, NB, scalars, n, cb, W, levels, NB, pts,
+             (const uint32_t*)dptr<uint32_t>(cur), dptr<uint64_t>(ent));
+    else
+      launch(c, ZK_K_MSM, 32.0 * n, 0, k_sort_scatter<kSortBinsSingle>, NB, scalars, n, cb, W, levels, NB, pts,
+             (const uint32_t*)dptr<uint32_t>(cur), dptr<uint64_t>(ent));
     launch(c, ZK_K_MSM, 0, 0, k_sort_fine, nbin, (const uint64_t*)dptr<uint64_t>(ent), bb, NB,
            (const uint32_t*)dptr<uint32_t>(cur), dptr<uint32_t>(cnt), dptr<uint32_t>(ord));
   }
@@ -581,9 +591,22 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
       auto work = [&](uint32_t w) {
         for (uint32_t i = w; i < nvars; i += nth) k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, tc[i].data()));
       };
+      // (a thread that cannot be created — std::system_error under a thread or
+      // resource limit — leaves its share to this thread: the workers already
+      // started are always joined, never destroyed joinable)
       std::vector<std::thread> pool;
-      for (uint32_t w = 1; w < nth; ++w) pool.emplace_back(work, w);
-      work(0);
+      std::vector<uint32_t> mine;
+      pool.reserve(nth);
+      mine.reserve(nth);
+      mine.push_back(0);
+      for (uint32_t w = 1; w < nth; ++w) {
+        try {
+          pool.emplace_back(work, w);
+        } catch (...) {
+          mine.push_back(w);
+        }
+      }
+      for (uint32_t w : mine) work(w);
       for (auto& th : pool) th.join();
     }
     // suffix bases L^(v)_j = L^(v+1)_j + L^(v+1)_(2^v + j) (eq sums to 1 over the

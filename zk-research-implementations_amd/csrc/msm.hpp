@@ -114,7 +114,13 @@ __host__ __device__ __forceinline__ uint32_t sort_block_pts(uint64_t n) {
   const uint64_t p = (n + 255) / 256;
   return (uint32_t)(p < 1024 ? 1024 : (p > kSortPts ? kSortPts : p));
 }
-constexpr uint32_t kSortBinsMax = 16896;    // Wt 2^C: c = 20: 13 x 1024; 20 batched levels of 10 bits: 520 x 32
+// coarse-bin tables in LDS (Wt 2^C entries): single MSMs need at most 13 x 1024
+// (c = 20); the level-batched pass up to 520 x 32 (20 levels of 10 bits).
+// k_sort_hist / k_sort_scatter are instantiated for both, so ordinary MSMs keep
+// the smaller table (occupancy of the sort passes).
+constexpr uint32_t kSortBinsSingle = 13312;
+constexpr uint32_t kSortBinsMax = 16896;
+static_assert(kSortBinsMax * 4 <= 160 * 1024, "the batched pass's bin table exceeds gfx950's LDS per workgroup");
 __host__ __device__ __forceinline__ uint32_t sort_fine_bits(uint32_t b) { return b / 2; }
 __host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t b) {
   const uint32_t F = sort_fine_bits(b), C = b - F;
@@ -127,10 +133,11 @@ __host__ __device__ __forceinline__ uint32_t bucket_slot(uint32_t key, uint32_t 
 __device__ __forceinline__ uint32_t point_window0(uint64_t i, uint32_t W, uint32_t levels) {
   return levels ? (63u - (uint32_t)__builtin_clzll(i + 1)) * W : 0u;
 }
+template <uint32_t BINS>
 __global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
                                                       uint32_t W, uint32_t levels, uint32_t NB, uint32_t pts,
                                                       uint32_t* __restrict__ H) {
-  __shared__ uint32_t hist[kSortBinsMax];
+  __shared__ uint32_t hist[BINS];
   const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = (levels ? levels * W : W) << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) hist[j] = 0;
   __syncthreads();
@@ -144,10 +151,11 @@ __global__ __launch_bounds__(kBlock) void k_sort_hist(const Fe* __restrict__ sca
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) H[(uint64_t)j * NB + blockIdx.x] = hist[j];
 }
+template <uint32_t BINS>
 __global__ __launch_bounds__(kBlock) void k_sort_scatter(const Fe* __restrict__ scalars, uint64_t n, uint32_t c,
                                                          uint32_t W, uint32_t levels, uint32_t NB, uint32_t pts,
                                                          const uint32_t* __restrict__ Hs, uint64_t* __restrict__ E) {
-  __shared__ uint32_t cur[kSortBinsMax];
+  __shared__ uint32_t cur[BINS];
   const uint32_t F = sort_fine_bits(c - 1), C = c - 1 - F, nbin = (levels ? levels * W : W) << C;
   for (uint32_t j = threadIdx.x; j < nbin; j += kBlock) cur[j] = Hs[(uint64_t)j * NB + blockIdx.x];
   __syncthreads();

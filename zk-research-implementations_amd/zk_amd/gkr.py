@@ -3,14 +3,18 @@ gkr/src/gkr_protocol.rs) over the C ABI: a layered circuit, `prove` (circuit
 evaluation, per-layer tables and sum-checks on the GPU) and `verify` (host).
 
 Differences from the reference:
-* the input layer's KZG step (gkr_protocol.rs:92-118) runs when `prove` is
-  given taus (BLS12-381 Fr, the reference's KZG field): the proof then carries
-  `input_proof` (commitment, both get_proofs, the opened values, the G2 taus)
-  and `verify` checks it with two KZG::verify pairings (:155-175). The
-  reference draws the taus from entropy (:97-103); they are the caller's here
-  so proofs are reproducible. Without taus the proof carries only the two
-  input-MLE evaluations KZG::open would return, and `verify` recomputes them
-  from the inputs when they are given;
+* the input layer's KZG step (gkr_protocol.rs:92-118) runs over BLS12-381 Fr
+  (the reference's KZG field, kzg.rs:3), as the reference always runs it: by
+  default (`taus="entropy"`) the taus are drawn from the OS entropy source like
+  the reference's `StdRng::from_entropy()` (:94-103) — a fresh, unreproducible
+  setup per proof — and caller-given taus make the proof reproducible (tests).
+  The proof then carries `input_proof` (commitment, both get_proofs, the opened
+  values, the G2 taus) and `verify` checks it with two KZG::verify pairings
+  (:155-175). `taus=None` skips the KZG step (a library extension, and the only
+  mode over BN254, whose reference `gkr::prove` cannot instantiate the
+  BLS12-381 KZG): the proof then carries only the two input-MLE evaluations
+  KZG::open would return, and `verify` recomputes them from the inputs when
+  they are given;
 * only the circuit shape for which the reference's table sizes agree is
   accepted (binary tree, powers of two, 1- or 2-gate output layer);
   anything else raises ValueError (the reference panics or mis-sizes).
@@ -18,6 +22,7 @@ Differences from the reference:
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from enum import IntEnum
 
@@ -102,11 +107,31 @@ def _layer_rounds(gates, coeffs, nco, ch, field):
     return polys, chal
 
 
+ENTROPY = "entropy"
+
+
+def entropy_taus(nvars: int, field: int = Field.BLS12_381_FR) -> list[int]:
+    """nvars field elements from the OS entropy source (the reference's
+    F::rand(StdRng::from_entropy()), gkr_protocol.rs:94-101): 512 random bits
+    reduced mod p each (bias < 2^-256)."""
+    p = modulus(field)
+    return [int.from_bytes(os.urandom(64), "little") % p for _ in range(nvars)]
+
+
 def prove(circuit: Circuit, inputs: list[int] | np.ndarray, ctx: Context | None = None,
-          taus: list[int] | None = None) -> GkrCircuitProof:  # :31-126
+          taus: list[int] | str | None = ENTROPY) -> GkrCircuitProof:  # :31-126
     """gkr::prove. inputs: canonical ints, or a uint64[n, 4] array of them
-    (little-endian limbs, the C ABI layout) which skips their conversion."""
+    (little-endian limbs, the C ABI layout) which skips their conversion.
+    taus: "entropy" (default; BLS12-381 Fr circuits run the input layer's KZG
+    step over a fresh setup drawn from os.urandom, like the reference, and
+    other fields skip it: the reference's KZG is BLS12-381-only), a list of
+    one tau per input variable (reproducible; BLS12-381 Fr only), or None (no
+    KZG step)."""
     ctx = ctx or default_context()
+    if isinstance(taus, str):
+        if taus != ENTROPY:
+            raise ValueError(f'taus must be a list, None or "{ENTROPY}"')
+        taus = entropy_taus(len(inputs).bit_length() - 1) if circuit.field == Field.BLS12_381_FR else None
     if taus is not None:
         return _prove_kzg(circuit, inputs, ctx, taus)
     gates, ops = circuit._abi()
@@ -181,7 +206,10 @@ def verify(proof: GkrCircuitProof, circuit: Circuit, inputs: list[int] | None = 
     pairing checks use proof.input_proof.g2_taus, as the reference does
     (gkr_protocol.rs:167,175): that setup must come from a trusted source the
     verifier holds. Taken from an untrusted prover it makes the check unsound
-    (a prover who picks its own setup can satisfy both pairings)."""
+    (a prover who picks its own setup can satisfy both pairings). Inputs, when
+    given, are checked as well: their MLE evaluations at the final points must
+    equal the opened values (without a KZG proof they are the only check of
+    the input layer)."""
     gates, ops = circuit._abi()
     total = _rounds(gates)
     flat = [p for layer in proof.proof_polynomials for p in layer]
@@ -202,7 +230,12 @@ def verify(proof: GkrCircuitProof, circuit: Circuit, inputs: list[int] | None = 
         return False
     claims = as_limbs(cl) if cl else np.zeros((1, 4), np.uint64)
     if proof.input_proof is not None:  # the reference's verifier: KZG checks, no inputs needed
-        return _verify_kzg(proof, circuit, gates, ops, coeffs, nco, claims)
+        if not _verify_kzg(proof, circuit, gates, ops, coeffs, nco, claims):
+            return False
+        if inputs is None:
+            return True
+        if tuple(proof.input_evaluations) != tuple(proof.input_proof.opened_evals):
+            return False
     x = as_limbs([int(v) for v in inputs]) if inputs is not None else None
     ok = C.c_int(0)
     _call(lib().zk_gkr_circuit_verify(int(circuit.field), REPR_CANONICAL, L, ptr(gates), ptr(ops),
