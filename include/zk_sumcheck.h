@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define ZK_ABI_VERSION 14u
+#define ZK_ABI_VERSION 15u
 
 typedef enum { ZK_BN254_FR = 0, ZK_BN254_FQ = 1, ZK_BLS12_381_FR = 2 } zk_field;
 typedef enum { ZK_REPR_CANONICAL = 0, ZK_REPR_MONTGOMERY = 1 } zk_repr;
@@ -245,6 +245,16 @@ int zk_kzg_commit(zk_ctx* ctx, const zk_kzg* kzg, zk_repr repr, const zk_fe* eva
 int zk_dev_kzg_commit(zk_ctx* ctx, const zk_kzg* kzg, const void* dev_evals /* Montgomery Fr */, zk_g1* out);
 int zk_kzg_get_proof(zk_ctx* ctx, const zk_kzg* kzg, zk_repr repr, const zk_fe* evals, const zk_fe* opened_value,
                      const zk_fe* point /* nvars */, zk_g1* out /* nvars */);
+/* KZG::get_proof with the evaluations already on the device (Montgomery Fr,
+ * 2^nvars, as zk_dev_kzg_commit takes them; read only): no host upload. repr
+ * applies to opened_value and point. */
+int zk_dev_kzg_get_proof(zk_ctx* ctx, const zk_kzg* kzg, zk_repr repr, const void* dev_evals, const zk_fe* opened_value,
+                         const zk_fe* point /* nvars */, zk_g1* out /* nvars */);
+/* Setups of >= 2^16 points use a fixed-base table of G1 (654 MB of device
+ * memory) built once per device and shared by every context of the process.
+ * This frees it for `device` (-1: every device); the next large setup rebuilds
+ * it (~50 ms). ZK_EINVAL while a setup on that device is using it. */
+int zk_kzg_release_fixed_base_cache(int device);
 int zk_msm_g1(zk_ctx* ctx, zk_repr repr, const zk_g1* bases, const zk_fe* scalars, size_t n, zk_g1* out);
 
 /* Verifier half (host, O(nvars) pairings; pcs/src/kzg_pcs/kzg.rs:35-49, :97-129).

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().zk_abi_version() == _lib.ABI_VERSION == 14
+    assert _lib.lib().zk_abi_version() == _lib.ABI_VERSION == 15
 
 
 def test_nm_exports_match_header():

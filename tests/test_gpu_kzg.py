@@ -327,3 +327,51 @@ def test_get_proof_level_batched_quotients(ctx, monkeypatch, batch):
         assert proof[i] == ko.mul(po.evaluate(R, q, taus[i + 1:]) if len(q) > 1 else q[0], ko.G1), (batch, i)
         cur = ko.get_remainder(cur, point[i])
     k.close()
+
+
+@pytest.mark.parametrize("n,batch", [(3, None), (12, None), (16, "6"), (20, "0")])
+def test_get_proof_device_resident_equals_host(ctx, monkeypatch, n, batch):
+    """zk_dev_kzg_get_proof (evaluations already in HBM, no upload) gives the
+    host entry point's proof, element for element, and KZG::verify accepts it;
+    the device table is left as it was (the reference's get_proof borrows f)."""
+    from zk_amd import Field
+
+    if batch is not None:
+        monkeypatch.setenv("ZK_PROOF_BATCH_LEVELS", batch)
+    rng = random.Random(700 + n)
+    taus = [rng.randrange(R) for _ in range(n)]
+    evals = [rng.randrange(R) for _ in range(1 << n)] if n > 3 else EVALS
+    point = [rng.randrange(R) for _ in range(n)]
+    k = KZG(taus, ctx)
+    v = k.open(point, evals)
+    t = ctx.upload(Field.BLS12_381_FR, evals)
+    try:
+        dev = k.get_proof_device(v, point, t)
+        assert dev == k.get_proof(v, point, evals)
+        assert KZG.verify(k.commit(evals), v, dev, point, k.g2_taus)
+        assert t.to_ints() == evals
+        with pytest.raises(ValueError):
+            k.get_proof_device(v, point, ctx.upload(Field.BLS12_381_FR, evals[: len(evals) // 2]))
+    finally:
+        t.free()
+        k.close()
+
+
+def test_release_fixed_base_cache_rebuilds(ctx):
+    """zk_kzg_release_fixed_base_cache (the 654 MB table large setups
+    share is no longer pinned for the process): after a release, the next
+    2^16-point setup rebuilds it and gives the same basis; releasing twice, or
+    a device with no table, is a no-op."""
+    from zk_amd.kzg import release_fixed_base_cache
+
+    rng = random.Random(16)
+    taus = [rng.randrange(R) for _ in range(16)]
+    evals = [rng.randrange(R) for _ in range(1 << 16)]
+    k = KZG(taus, ctx)
+    c0 = k.commit(evals)
+    k.close()
+    release_fixed_base_cache()
+    release_fixed_base_cache(0)
+    k = KZG(taus, ctx)
+    assert k.commit(evals) == c0 == ko.mul(po.evaluate(R, evals, taus), ko.G1)
+    k.close()

@@ -5,6 +5,7 @@
 # its library built), REPS rounds. Prints ms per proof with and without the
 # per-launch events, and the event-timed launches.
 # usage (inside gpurun, from the repo root): bash tools/ab_trees.sh abtest/r4tree [...]
+# (EXTRA="--force-rccl": extra bench.py arguments for every run; NOEV=0: events only)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
@@ -12,8 +13,10 @@ root=$PWD
 SIDE="--no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-plain --no-config4"
 for rep in $(seq 1 ${REPS:-4}); do
   for tree in "." "$@"; do
-    for ev in "" "--no-events"; do
-      (cd "$root/$tree" && timeout -k 10 180 python3 bench.py --steps 100 --warmup 20 $SIDE $ev \
+    evs=("" "--no-events")
+    [ "${NOEV:-1}" = "0" ] && evs=("")
+    for ev in "${evs[@]}"; do
+      (cd "$root/$tree" && timeout -k 10 180 python3 bench.py --steps 100 --warmup 20 $SIDE $EXTRA $ev \
         > "$root/gpurun_out/abt.json" 2> "$root/gpurun_out/abt.err") || { tail -20 gpurun_out/abt.err; exit 1; }
       python3 -c "
 import json, sys

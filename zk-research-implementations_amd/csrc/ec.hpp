@@ -13,6 +13,8 @@
 // the exceptional cases (P = Q, P = -Q, infinity) handled explicitly, so the
 // group element — and hence the canonical affine output — is exact.
 #pragma once
+#include <string.h>
+
 #include "field.hpp"
 
 namespace zk {
@@ -93,8 +95,55 @@ ZK_HD Fq fq_sub(const Fq& a, const Fq& b) {
 ZK_HD Fq fq_dbl(const Fq& a) { return fq_add(a, a); }
 ZK_HD Fq fq_neg(const Fq& a) { return fq_sub(fq_zero(), a); }
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host: the same product on 6 x 64-bit limbs (unsigned __int128 rows, CIOS),
+// ~4x fewer instructions than the 32-bit rows below — the host's G1/G2 work
+// (the MSMs' window Horners, the setup's G2 taus, point normalisation, the
+// pairings) is chains of these. Same value: the fully reduced a b 2^-384 mod p.
+namespace fqh {
+using u128 = unsigned __int128;
+constexpr uint64_t P(int i) { return (uint64_t)Bls12_381Fq::P[2 * i] | ((uint64_t)Bls12_381Fq::P[2 * i + 1] << 32); }
+constexpr uint64_t pinv() {  // -p^-1 mod 2^64 (Newton)
+  uint64_t x = 1;
+  for (int i = 0; i < 7; ++i) x *= 2 - P(0) * x;
+  return (uint64_t)0 - x;
+}
+inline Fq mul(const Fq& a, const Fq& b) {
+  uint64_t A[6], B[6], t[7] = {0, 0, 0, 0, 0, 0, 0};
+  memcpy(A, a.v, 48);
+  memcpy(B, b.v, 48);
+  for (int i = 0; i < 6; ++i) {
+    uint64_t c = 0;
+    for (int j = 0; j < 6; ++j) {
+      const u128 x = (u128)A[j] * B[i] + t[j] + c;
+      t[j] = (uint64_t)x;
+      c = (uint64_t)(x >> 64);
+    }
+    const uint64_t t6 = t[6] + c;  // (t < 2p < 2^382 between rows: no overflow)
+    const uint64_t m = t[0] * pinv();
+    u128 x = (u128)m * P(0) + t[0];
+    c = (uint64_t)(x >> 64);
+    for (int j = 1; j < 6; ++j) {
+      x = (u128)m * P(j) + t[j] + c;
+      t[j - 1] = (uint64_t)x;
+      c = (uint64_t)(x >> 64);
+    }
+    x = (u128)t6 + c;
+    t[5] = (uint64_t)x;
+    t[6] = (uint64_t)(x >> 64);
+  }
+  Fq r;
+  memcpy(r.v, t, 48);
+  return fq_reduce_once(r);  // (t < 2p)
+}
+}  // namespace fqh
+#endif
+
 // CIOS Montgomery product a*b*2^-384 mod p (invariant t < 2p < 2^384 between rows)
 ZK_HD Fq fq_mul(const Fq& a, const Fq& b) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return fqh::mul(a, b);
+#endif
   uint32_t t[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) t[j] = 0;

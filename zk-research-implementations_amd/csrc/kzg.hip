@@ -105,6 +105,37 @@ G1J* seg_reduce(zk_ctx* c, const G1A* bases, uint64_t nbases, const uint32_t* or
   }
 }
 
+// fn(0 .. n-1) on up to kHostThreads host threads (the box gives a GPU 16
+// CPUs): independent chains of host group operations — Horners over window
+// sums, G2 scalar multiplications. A thread that cannot be created leaves its
+// share to the calling thread; every thread started is joined.
+constexpr uint32_t kHostThreads = 16;
+template <class Fn>
+void host_parallel(uint32_t n, Fn&& fn) {
+  const uint32_t nth = std::min<uint32_t>(n, kHostThreads);
+  if (nth <= 1) {
+    for (uint32_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  auto work = [&](uint32_t w) {
+    for (uint32_t i = w; i < n; i += nth) fn(i);
+  };
+  std::vector<std::thread> pool;
+  std::vector<uint32_t> mine;
+  pool.reserve(nth);
+  mine.reserve(nth);
+  mine.push_back(0);
+  for (uint32_t w = 1; w < nth; ++w) {
+    try {
+      pool.emplace_back(work, w);
+    } catch (...) {
+      mine.push_back(w);
+    }
+  }
+  for (uint32_t w : mine) work(w);
+  for (auto& th : pool) th.join();
+}
+
 // a small MSM's time is one thread's serial chain of group additions: the
 // per-thread work of the bucket and window sums shrinks until at least this
 // many threads run (2 waves per SIMD of a 256-CU MI355X)
@@ -292,7 +323,9 @@ std::vector<G1J> msm_levels(zk_ctx* c, const G1A* bases, const Fe* scalars, uint
   uint32_t W = 0, cb = 0;
   const std::vector<G1J> S = msm_window_sums(c, bases, scalars, ((uint64_t)1 << levels) - 1, levels, W, cb);
   std::vector<G1J> out(levels);
-  for (uint32_t v = 0; v < levels; ++v) out[v] = windows_horner(S.data() + (size_t)v * W, W, cb);
+  // each level's Horner is a serial chain of ~W cb host doublings (250 at 20
+  // levels of 10-bit windows): the levels run on host threads
+  host_parallel(levels, [&](uint32_t v) { out[v] = windows_horner(S.data() + (size_t)v * W, W, cb); });
   return out;
 }
 
@@ -365,14 +398,19 @@ const G1A* g1_fixed_table16(zk_ctx* c) {
 // every context on the device shares it (654 MB, kept until the process
 // exits — it depends on nothing but the curve's generator). Round 4 rebuilt
 // it per context (cold setup 125 ms against 76 ms warm).
+// zk_kzg_release_fixed_base_cache frees an entry; a setup holds a
+// lease on its device's entry (`users`) from the lookup until its fixed-base
+// kernel has finished, and a release refuses while one is held.
 struct FixedBaseCache {
   std::mutex m;
-  std::map<int, void*> table20;  // device -> affine table (never freed: process lifetime)
+  std::map<int, void*> table20;  // device -> affine table (until released)
+  std::map<int, int> users;      // device -> setups using the table now
 };
 FixedBaseCache& fixed_base_cache() {
   static FixedBaseCache* cache = new FixedBaseCache();  // (leaked on purpose: no teardown order with the HIP runtime)
   return *cache;
 }
+// (the caller holds a lease: FixedBaseLease)
 const G1A* g1_fixed_table20(zk_ctx* c) {
   using namespace zk;
   FixedBaseCache& fc = fixed_base_cache();
@@ -398,6 +436,23 @@ const G1A* g1_fixed_table20(zk_ctx* c) {
   fc.table20[c->device] = t20.p;
   return dptr<G1A>(t20);
 }
+struct FixedBaseLease {  // a setup's use of its device's table20 (see FixedBaseCache)
+  zk_ctx* c;
+  int device;
+  explicit FixedBaseLease(zk_ctx* cc) : c(cc), device(cc->device) {
+    FixedBaseCache& fc = fixed_base_cache();
+    std::lock_guard<std::mutex> lock(fc.m);
+    fc.users[device] += 1;
+  }
+  ~FixedBaseLease() {
+    (void)hipStreamSynchronize(c->stream);  // (an unwinding setup: its kernel has finished reading the table)
+    FixedBaseCache& fc = fixed_base_cache();
+    std::lock_guard<std::mutex> lock(fc.m);
+    fc.users[device] -= 1;
+  }
+  FixedBaseLease(const FixedBaseLease&) = delete;
+  FixedBaseLease& operator=(const FixedBaseLease&) = delete;
+};
 // below this many basis points a setup uses the 8-bit table (k_fixed_base8:
 // 32 mixed additions per point) instead of building / holding table20
 constexpr uint64_t kSetupTable20Min = 1ull << 16;
@@ -557,6 +612,8 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
     k->device = c->device;
     const uint64_t N = (uint64_t)1 << nvars, total = 2 * N - 1;  // every suffix level, level v at 2^v - 1
     const bool big = N >= kSetupTable20Min;
+    std::unique_ptr<FixedBaseLease> lease;  // (held until this setup's kernels have finished)
+    if (big) lease = std::make_unique<FixedBaseLease>(c);
     const G1A* table = big ? g1_fixed_table20(c) : g1_fixed_table(c);
     DevBuf& tb = c->msm[14];
     tb.ensure(nvars * 32);
@@ -580,34 +637,14 @@ int zk_kzg_setup(zk_ctx* c, zk_repr repr, const zk_fe* taus, uint32_t nvars, zk_
              (const Fe*)sc.p, N, J + (N - 1));
     // G2 half of run_trusted_setup (:43-46): tau_i * G2, on the host (nvars
     // scalar multiplications) while the basis kernels run
-    // (split over up to 8 host threads; the scalars are converted and checked
-    // on this thread first, so nothing below can throw)
+    // (on up to kHostThreads host threads; the scalars are converted and
+    // checked on this thread first, so nothing below can throw)
     {
       const zk::G2J g2 = zk::g2_from_affine(zk::g2_generator());
       std::vector<std::array<uint32_t, 8>> tc(nvars);
       for (uint32_t i = 0; i < nvars; ++i) fr_canon(repr, taus[i], tc[i].data());
       k->g2_taus.resize(nvars);
-      const uint32_t nth = std::min<uint32_t>(nvars, 8);
-      auto work = [&](uint32_t w) {
-        for (uint32_t i = w; i < nvars; i += nth) k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, tc[i].data()));
-      };
-      // (a thread that cannot be created — std::system_error under a thread or
-      // resource limit — leaves its share to this thread: the workers already
-      // started are always joined, never destroyed joinable)
-      std::vector<std::thread> pool;
-      std::vector<uint32_t> mine;
-      pool.reserve(nth);
-      mine.reserve(nth);
-      mine.push_back(0);
-      for (uint32_t w = 1; w < nth; ++w) {
-        try {
-          pool.emplace_back(work, w);
-        } catch (...) {
-          mine.push_back(w);
-        }
-      }
-      for (uint32_t w : mine) work(w);
-      for (auto& th : pool) th.join();
+      host_parallel(nvars, [&](uint32_t i) { k->g2_taus[i] = zk::g2_to_affine(zk::g2_mul(g2, tc[i].data())); });
     }
     // suffix bases L^(v)_j = L^(v+1)_j + L^(v+1)_(2^v + j) (eq sums to 1 over the
     // dropped variable), Jacobian, then ONE batch normalisation of all levels:
@@ -681,7 +718,45 @@ int zk_kzg_get_proof(zk_ctx* c, const zk_kzg* k, zk_repr repr, const zk_fe* eval
     for (uint32_t i = 0; i < k->nv; ++i) pt[i] = in_mont<Fr381>(repr, point[i]);
     std::vector<G1J> q;
     kzg_get_proof(c, k, c->input.fe(), in_mont<Fr381>(repr, *opened_value), pt, q);
-    for (uint32_t i = 0; i < k->nv; ++i) out[i] = g1_out(q[i]);
+    const std::vector<G1A> qa = host_normalize(q);  // (one inversion for all nv points)
+    for (uint32_t i = 0; i < k->nv; ++i) out[i] = g1a_out(qa[i]);
+  });
+}
+
+int zk_dev_kzg_get_proof(zk_ctx* c, const zk_kzg* k, zk_repr repr, const void* dev_evals, const zk_fe* opened_value,
+                         const zk_fe* point, zk_g1* out) {
+  return guarded([&] {
+    require(c && k && dev_evals && opened_value && point && out, "null argument");
+    bind(c);
+    std::vector<Fe> pt(k->nv);
+    for (uint32_t i = 0; i < k->nv; ++i) pt[i] = in_mont<Fr381>(repr, point[i]);
+    std::vector<G1J> q;
+    kzg_get_proof(c, k, reinterpret_cast<const Fe*>(dev_evals), in_mont<Fr381>(repr, *opened_value), pt, q);
+    const std::vector<G1A> qa = host_normalize(q);
+    for (uint32_t i = 0; i < k->nv; ++i) out[i] = g1a_out(qa[i]);
+  });
+}
+
+int zk_kzg_release_fixed_base_cache(int device) {
+  return guarded([&] {
+    FixedBaseCache& fc = fixed_base_cache();
+    std::lock_guard<std::mutex> lock(fc.m);
+    int cur = 0;
+    HIPCK(hipGetDevice(&cur));
+    struct Restore {
+      int d;
+      ~Restore() { (void)hipSetDevice(d); }
+    } restore{cur};
+    for (auto it = fc.table20.begin(); it != fc.table20.end();) {
+      if (device >= 0 && it->first != device) {
+        ++it;
+        continue;
+      }
+      require(fc.users[it->first] == 0, "a KZG setup on this device is using the fixed-base table");
+      HIPCK(hipSetDevice(it->first));
+      HIPCK(hipFree(it->second));
+      it = fc.table20.erase(it);
+    }
   });
 }
 

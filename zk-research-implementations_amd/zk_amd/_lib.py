@@ -17,7 +17,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 ZK_OK, ZK_EINVAL, ZK_EDEVICE, ZK_ECOMM, ZK_ENOMEM, ZK_EUNSUPPORTED = range(6)
 ZK_BLOB_GKR, ZK_BLOB_SUMCHECK = 1, 2
 ERROR_NAMES = {1: "ZK_EINVAL", 2: "ZK_EDEVICE", 3: "ZK_ECOMM", 4: "ZK_ENOMEM", 5: "ZK_EUNSUPPORTED"}
-ABI_VERSION = 14  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
+ABI_VERSION = 15  # ZK_ABI_VERSION in include/zk_sumcheck.h: the ZkStats layout and the signatures below
 KERNEL_KINDS = ["gkr_round0", "gkr_round", "sc_round", "fold", "reduce", "convert", "synth", "layer", "msm", "gkr_round_lanes", "gkr_tail", "gkr_dround", "gkr_dtail", "gkr_d0", "gkr_dm", "gkr_t33", "coll"]
 
 
@@ -87,6 +87,8 @@ SIGNATURES = {
     "zk_kzg_commit": (I, [P, P, I, P, P]),
     "zk_dev_kzg_commit": (I, [P, P, P, P]),
     "zk_kzg_get_proof": (I, [P, P, I, P, P, P, P]),
+    "zk_dev_kzg_get_proof": (I, [P, P, I, P, P, P, P]),
+    "zk_kzg_release_fixed_base_cache": (I, [I]),
     "zk_msm_g1": (I, [P, I, P, P, SZ, P]),
     "zk_kzg_g2_taus": (I, [P, P]),
     "zk_kzg_verify": (I, [I, P, P, P, U32, P, U32, P, C.POINTER(C.c_int)]),

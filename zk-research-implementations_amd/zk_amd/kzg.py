@@ -124,6 +124,25 @@ class KZG:  # kzg.rs:10-49
         return _points(out)
 
 
+    def get_proof_device(self, opened_value: int, opening_values: list[int], table) -> list:
+        """get_proof over evaluations already on the device (a DeviceTable of
+        2^nvars BLS12-381 Fr values, e.g. Context.upload / synth): no host
+        upload (zk_dev_kzg_get_proof)."""
+        if table.count != 1 << self.nvars or int(table.field) != int(FIELD):
+            raise ValueError("the device table must hold 2^nvars BLS12-381 Fr values")
+        out = np.zeros((self.nvars, 12), np.uint64)
+        _call(lib().zk_dev_kzg_get_proof(self.ctx.h, self.h, REPR_CANONICAL, table.ptr,
+                                         ptr(as_limbs([int(opened_value)])),
+                                         ptr(as_limbs([int(v) for v in opening_values])), ptr(out)))
+        return _points(out)
+
+
+def release_fixed_base_cache(device: int = -1) -> None:
+    """Free the per-device fixed-base table large setups share (654 MB of HBM;
+    -1: every device). ZkError while a setup is using it."""
+    _call(lib().zk_kzg_release_fixed_base_cache(int(device)))
+
+
 def msm_g1(bases: list, scalars: list[int], ctx: Context | None = None):
     """sum_i scalars[i] * bases[i] (bases must be on the curve)."""
     ctx = ctx or default_context()
