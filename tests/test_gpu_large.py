@@ -120,6 +120,23 @@ def test_t33_pipelined_and_plain_loops_match_oracle(monkeypatch, pipe, cap):
         c.close()
 
 
+def test_oct32_second_pass_headline_matches_fixture(monkeypatch):
+    """Round 6 made the 64-octant k_gkr_t33 the default wherever a level has a
+    chunk per CU (ZK_T33_OCT64_MIN 4 -> 1: the second pass, level 6 at 24
+    variables, now pipelined 64-octant). The 32-octant path keeps the smaller
+    levels; with the old threshold it takes the second pass again, which must
+    still give the committed headline proof."""
+    g = LARGE["bn254_fr_24_s3"]
+    monkeypatch.setenv("ZK_T33_OCT64_MIN", "4")
+    c = zk_amd.Context(0)
+    try:
+        polys, chal = device_proof(c, 0, 24, 3)
+    finally:
+        c.close()
+    assert chal == [h2i(x) for x in g["challenges"]]
+    assert blob_digest(0, polys, chal) == g["blob_keccak256"]
+
+
 def test_grid_capped_headline_matches_fixture(monkeypatch):
     g = LARGE["bn254_fr_24_s3"]
     monkeypatch.setenv("ZK_GRID_CAP", "37")  # every step several chunks per block, odd grids

@@ -14,5 +14,9 @@ B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fold --no-e2e --
 # host; the kernels' work is identical either way.
 export ZK_PRELAUNCH=0
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- $B > gpurun_out/prof_${TAG}_bench.json 2> gpurun_out/prof_${TAG}.err
+# the product schedule itself: pre-enqueued steps, the
+# persistent k_gkr_dtail and the host rounds, exactly what bench.py runs; each
+# pre-enqueued kernel's duration then includes its wait for the challenge
+ZK_PRELAUNCH=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_product -o run -- $B > gpurun_out/prof_${TAG}_product_bench.json 2>> gpurun_out/prof_${TAG}.err
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_${TAG}_fetch -o run -- $B > /dev/null 2>> gpurun_out/prof_${TAG}.err
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_${TAG}_write -o run -- $B > /dev/null 2>> gpurun_out/prof_${TAG}.err

@@ -1,12 +1,11 @@
 set -o pipefail
-# round 6 session 5: KZG host arithmetic (64-bit Fq rows, threaded Horners, batch-normalised proofs):
-# the KZG tests, the parts at 2^10..2^16, config 5's leg; then the first t33's SQ counters vs its pattern
-timeout -k 10 700 python -u -m pytest tests/test_gpu_kzg.py tests/test_gpu_gkr_circuit.py tests/test_pairing_cpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/s5_tests.log 2>&1 || { tail -30 gpurun_out/s5_tests.log; exit 1; }
-tail -2 gpurun_out/s5_tests.log
-timeout -k 10 300 python tools/kzg_parts.py > gpurun_out/kzg_parts2.log 2>&1 || { tail gpurun_out/kzg_parts2.log; exit 1; }
-cat gpurun_out/kzg_parts2.log
-timeout -k 10 600 python bench.py --no-cpu-baseline --no-fold --no-e2e --no-plain --no-config4 --steps 5 --warmup 2 > gpurun_out/kzg5.json 2> gpurun_out/kzg5.err || { tail gpurun_out/kzg5.err; exit 1; }
+# round 6 session 7: the whole GPU suite + smoke on this tree, the default bench line, the rocprof profile
+timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r6_pytest_gpu.txt 2>&1 || { tail -30 gpurun_out/r6_pytest_gpu.txt; exit 1; }
+tail -2 gpurun_out/r6_pytest_gpu.txt
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" >> gpurun_out/r6_pytest_gpu.txt 2>&1 || { tail gpurun_out/r6_pytest_gpu.txt; exit 1; }
+tail -1 gpurun_out/r6_pytest_gpu.txt
+timeout -k 10 600 python bench.py > gpurun_out/r6_bench.json 2> gpurun_out/r6_bench.err || { tail gpurun_out/r6_bench.err; exit 1; }
 python3 -c "
-import json; d=json.load(open('gpurun_out/kzg5.json')); k=d['config5_bls12_381']; print({x: k[x] for x in k if x.endswith('_ms') or 'verified' in x}); print(d.get('gkr_circuit_kzg'))"
-bash tools/pmc_t33.sh || exit 1
-python3 tools/pmc_t33_summary.py gpurun_out/pmct33_k1 gpurun_out/pmct33_k2 gpurun_out/pmct33_m1 gpurun_out/pmct33_m2
+import json; d=json.load(open('gpurun_out/r6_bench.json')); r=d['roofline']; print(d['ms_per_step'], d['value']/1e9, r['frac'], r['avg_launch_us'], [(x['kind'], x['us']) for x in r['launches_of_proof']]); k=d['config5_bls12_381']; print({x: k[x] for x in k if x.endswith('_ms')}); print(d['gkr_circuit_kzg']['ms_median'], d['gkr_circuit']['ms_median'], d['config4_26var']['ms_median'], d['cpu_baseline']['value'])"
+bash tools/profile_bench.sh r6 || { tail gpurun_out/prof_r6.err; exit 1; }
+echo profile ok

@@ -224,7 +224,7 @@ struct zk_ctx {
   uint32_t gather_vars = 10;  // sharded: gather the tables once <= this many local rounds remain, finish locally (ZK_GATHER_VARS; 0: at the end)
   DevBuf gbuf;                // sharded gather: fold scratch, the one-hot buffer, the interleaved global tables
   bool t33_pipe = true;  // ZK_T33_PIPE (0: off): the 64-octant k_gkr_t33 with a double-buffered image, products interleaved
-  uint32_t t33_oct64_min = 4;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks)
+  uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks; round 6: 4 -> 1, the second pass 2 us faster, profiles/r6_knob_ab.txt)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
   bool device_fs = false;    // the persistent tail draws its own challenges (ZK_DEVICE_FS; dfs.hpp)
@@ -250,10 +250,6 @@ struct zk_ctx {
   std::vector<void*> peer_open;       // the peers' buffers, opened from their IPC handles
   zk::PeerSlots* d_peer = nullptr;    // device copy of the slot table
   uint64_t peer_seq = 0;              // last reduction's sequence tag (the same on every rank)
-  // RCCL steps: the publish of the last all-reduce not yet enqueued (host.hpp
-  // take_publish / flush_publish), and whether the next step may take it
-  bool pub_pending = false, defer_publish = false;
-  uint32_t pub_n = 0, pub_tag = 0;
   // KZG / MSM scratch (grow-only) and the cached fixed-base table of G1
   DevBuf msm[19];
   bool msm_balanced = true;  // ZK_MSM_BALANCED: bucket sums in equal tasks across bucket boundaries (kzg.hip)
@@ -658,38 +654,20 @@ inline void wait_flag(zk_ctx* c, uint32_t tag) {
 // product sums, L = 8: element sums), summed over ranks when sharded.
 // Stream side of a round's hand-off, enqueued right after its kernel: across
 // ranks over RCCL the device totals are all-reduced and then published.
-// With pre-enqueued steps (defer_publish) the publish of the all-reduced sums
-// is left to the next step kernel's block 0 (DIn::pub_*, kernels.hpp
-// wave_publish): take_publish hands it over, flush_publish launches k_publish
-// for a publish no kernel took (the phase's last step, or a next step without
-// a DIn). One kernel and one boundary fewer per sharded step.
-inline void flush_publish(zk_ctx* c) {
-  if (!c->pub_pending) return;
-  c->pub_pending = false;
-  zk::k_publish<<<1, 256, 0, c->stream>>>(d_red(c), (int)c->pub_n, c->h_red, h_flag(c), c->pub_tag);
-  HIPCK(hipGetLastError());
-}
-inline void take_publish(zk_ctx* c, zk::DIn& din) {
-  if (!c->pub_pending) return;
-  c->pub_pending = false;
-  din.pub_src = d_red(c);
-  din.pub_dst = c->h_red;
-  din.pub_flag = h_flag(c);
-  din.pub_n = c->pub_n;
-  din.pub_tag = c->pub_tag;
-}
+// (Round 6 measured leaving the publish to the next pre-enqueued step kernel's
+// block 0 instead of k_publish — one kernel and one boundary fewer per step —
+// and removed it: that block's copy then waits behind the step's first loads,
+// which every other block issues at entry, and the forced-RCCL proof at world 1
+// got 5-8 us slower, profiles/r6_rccl_publish_ab.txt.)
 inline void enqueue_reduce(zk_ctx* c, const zk::RoundSink& sk, bool across_ranks, int n) {
   if (across_ranks && multi_rank(c) && c->comm == COMM_RCCL && !c->peer) {
-    flush_publish(c);  // (d_red is about to be overwritten)
     {
       CollTimer ct(c, 8.0 * n);
       NCCLCK(ncclAllReduce(d_red(c), d_red(c), n, ncclUint64, ncclSum, c->nccl, c->stream));
     }
     c->stats.collectives += 1;
-    c->pub_pending = true;
-    c->pub_n = (uint32_t)n;
-    c->pub_tag = sk.tag;
-    if (!c->defer_publish) flush_publish(c);
+    zk::k_publish<<<1, 256, 0, c->stream>>>(d_red(c), n, c->h_red, h_flag(c), sk.tag);
+    HIPCK(hipGetLastError());
   }
 }
 
@@ -1120,7 +1098,6 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.relay = d_rpost(c);
         din.err = h_err(c);
         din.tag = rtags[si] = ++c->rtag;
-        take_publish(c, din);
       } else {
         din.ra = rz;
         din.rb = ra;
@@ -1231,7 +1208,6 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
         din.relay = d_rpost(c);
         din.err = h_err(c);
         din.tag = rtags[si] = ++c->rtag;
-        take_publish(c, din);
       } else if (st.np == 2) {
         din.ra = ra;
         din.rb = rb;
@@ -1293,19 +1269,10 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
   PostR post{c};
   if (pre) {
     const auto t0 = std::chrono::steady_clock::now();
-    struct DeferGuard {  // (an exception mid-enqueue leaves nothing deferred for the next call)
-      zk_ctx* c;
-      ~DeferGuard() { c->defer_publish = false; c->pub_pending = false; }
-    } dg{c};
-    c->defer_publish = true;  // (a step's publish rides on the next step kernel, take_publish)
     for (size_t si = 0; si < ns; ++si) {
-      const int k = steps[si].kind;
-      if (k != GS_T33 && k != GS_T32 && k != GS_DOUBLE) flush_publish(c);  // (kernels without a DIn)
       enqueue(si);
       post.last = last_tag(si);  // from here on the guard releases what is enqueued
     }
-    c->defer_publish = false;
-    flush_publish(c);
     if (getenv("ZK_DEBUG_ENQUEUE"))
       fprintf(stderr, "zk: enqueued %zu steps (%u rounds) in %.1f us\n", ns, nv,
               std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());

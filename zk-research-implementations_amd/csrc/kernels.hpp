@@ -964,24 +964,7 @@ struct DIn {
   RPost* relay;        // device relay slot (used when gridDim > 1)
   uint32_t* err;       // pinned error word
   uint32_t tag;
-  // the previous step's publish, when it was all-reduced over RCCL on the
-  // stream right before this pre-enqueued kernel (host.hpp enqueue_reduce):
-  // block 0's wave 0 copies pub_n u64 from pub_src (device) to pub_dst (pinned)
-  // and raises *pub_flag = pub_tag before it polls for its own challenges — the
-  // k_publish kernel (and its boundary) of the non-deferred form, folded in
-  const uint64_t* pub_src;
-  uint64_t* pub_dst;
-  uint32_t* pub_flag;
-  uint32_t pub_n, pub_tag;
 };
-// wave 0 (all 64 lanes): the deferred publish of DIn (pub_src != null)
-__device__ __forceinline__ void wave_publish(const DIn& in) {
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t i = lane; i < in.pub_n; i += 64)
-    __hip_atomic_store(in.pub_dst + i, in.pub_src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's stores drained before the flag (one wave: in order)
-  if (lane == 0) __hip_atomic_store(in.pub_flag, in.pub_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 // NV tagged values (8 words each) into s_w[8 NV] (LDS; valid after the barrier).
 // Block 0 polls the host slot and copies the words to the device relay when
 // `relay`; the other blocks poll the relay. dev_only: every block polls the
@@ -993,7 +976,6 @@ __device__ __forceinline__ void block_get_words(const DIn& in, uint32_t* s_w, bo
     const bool mine = lane < 8 * NV;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const bool direct = blockIdx.x == 0 && !dev_only;
-    if (direct && in.pub_src) wave_publish(in);
     uint64_t v = 0;
     bool ok = true;
     while (true) {

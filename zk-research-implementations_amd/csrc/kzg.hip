@@ -838,18 +838,31 @@ int zk_kzg_verify(zk_repr repr, const zk_g1* commitment, const zk_fe* opened_val
     uint32_t v[8];
     fr_canon(repr, *opened_value, v);
     const G1J lhs = g1_add(g1_from_affine(parse_g1(*commitment)), g1_neg(g1_mul(g1, v)));
-    std::vector<G1A> P{g1_affine(lhs)};
-    std::vector<G2A> Q{g2_generator()};
+    // inputs parsed and checked on this thread (they may throw); the G2 factors
+    // and the Miller loops — independent per point — on host threads, then
+    // one product and one final exponentiation (multi_pairing's value)
+    std::vector<G1A> P(npoint + 1);
+    std::vector<G2A> Q(npoint + 1), tau(npoint);
+    std::vector<std::array<uint32_t, 8>> a(npoint);
+    P[0] = g1_affine(lhs);
+    Q[0] = g2_generator();
     for (uint32_t i = 0; i < npoint; ++i) {
-      uint32_t a[8];
-      fr_canon(repr, point[i], a);
-      const G2J factor = g2_add(g2_from_affine(parse_g2(g2_taus[i])), g2_neg(g2_mul(g2, a)));
+      fr_canon(repr, point[i], a[i].data());
+      tau[i] = parse_g2(g2_taus[i]);
       G1A qi = parse_g1(proof[i]);
       if (!g1a_is_inf(qi)) qi.y = fq_neg(qi.y);
-      P.push_back(qi);
-      Q.push_back(g2_to_affine(factor));
+      P[i + 1] = qi;
     }
-    *out_verified = fq12_is_one(multi_pairing(P, Q)) ? 1 : 0;
+    host_parallel(npoint, [&](uint32_t i) {
+      Q[i + 1] = g2_to_affine(g2_add(g2_from_affine(tau[i]), g2_neg(g2_mul(g2, a[i].data()))));
+    });
+    std::vector<Fq12> ml(npoint + 1, fq12_one());
+    host_parallel(npoint + 1, [&](uint32_t i) {
+      if (!g1a_is_inf(P[i]) && !Q[i].inf) ml[i] = miller_loop(P[i], Q[i]);
+    });
+    Fq12 f = fq12_one();
+    for (const Fq12& m : ml) f = fq12_mul(f, m);
+    *out_verified = fq12_is_one(final_exponentiation(f)) ? 1 : 0;
   });
 }
 
