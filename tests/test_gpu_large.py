@@ -137,6 +137,35 @@ def test_oct32_second_pass_headline_matches_fixture(monkeypatch):
     assert blob_digest(0, polys, chal) == g["blob_keccak256"]
 
 
+@pytest.mark.parametrize("order", ["1", "2"])
+@pytest.mark.parametrize("case", [("oracle", 20, "0"), ("oracle", 21, "5"), ("fixture", 24, "0"), ("fixture", 26, "0")])
+def test_mall_order_matches(monkeypatch, case, order):
+    """ZK_MALL_ORDER=1: k_gkr_d0t takes its chunks grouped by the first
+    k_gkr_t33's chunks and that t33 walks them in reverse; 2: the groups also
+    permuted so the first t33's last outputs are whole input sets of the
+    second's first chunks (only the order of exact integer sums and of
+    independent folds changes): the oracle's proof at
+    20 and 21 variables (21 with grid-capped blocks, several chunks each), and
+    the committed fixtures at 24 and 26."""
+    kind, n, cap = case
+    monkeypatch.setenv("ZK_MALL_ORDER", order)
+    if cap != "0":
+        monkeypatch.setenv("ZK_GRID_CAP", cap)
+    c = zk_amd.Context(0)
+    try:
+        seed = {24: 3, 26: 4}.get(n, 23)
+        got = device_proof(c, 0, n, seed)
+    finally:
+        c.close()
+    if kind == "oracle":
+        assert got == oracle_proof(0, n, seed)
+    else:
+        g = LARGE[f"bn254_fr_{n}_s{seed}"]
+        polys, chal = got
+        assert chal == [h2i(x) for x in g["challenges"]]
+        assert blob_digest(0, polys, chal) == g["blob_keccak256"]
+
+
 def test_grid_capped_headline_matches_fixture(monkeypatch):
     g = LARGE["bn254_fr_24_s3"]
     monkeypatch.setenv("ZK_GRID_CAP", "37")  # every step several chunks per block, odd grids

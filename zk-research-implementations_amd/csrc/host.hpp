@@ -224,6 +224,7 @@ struct zk_ctx {
   uint32_t gather_vars = 10;  // sharded: gather the tables once <= this many local rounds remain, finish locally (ZK_GATHER_VARS; 0: at the end)
   DevBuf gbuf;                // sharded gather: fold scratch, the one-hot buffer, the interleaved global tables
   bool t33_pipe = true;  // ZK_T33_PIPE (0: off): the 64-octant k_gkr_t33 with a double-buffered image, products interleaved
+  uint32_t mall_order = 0;  // ZK_MALL_ORDER: k_gkr_d0t reads the first k_gkr_t33's chunks grouped, that t33 walks them in reverse; 2: the groups permuted for the second t33 too (mfma.hpp)
   uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks; round 6: 4 -> 1, the second pass 2 us faster, profiles/r6_knob_ab.txt)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
   uint64_t* h_tab = nullptr; // pinned, device-mapped: the 4 tables handed to the host rounds
@@ -1045,6 +1046,16 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     if (next != end) fail(ZK_EINVAL, "internal: step schedule does not cover every round");
   }
+  // ZK_MALL_ORDER: the input pass groups its chunks by the first 64-octant
+  // k_gkr_t33's (16 of its 32-octant chunks per t33 chunk), that t33 takes them
+  // in reverse (mfma.hpp k_gkr_d0t / k_gkr_t33 `order`); needs both steps at
+  // these positions and the input pass's chunk count a multiple of 16
+  const bool oct64_3 = (L >> 6) / 64 >= (uint64_t)c->num_cus * c->t33_oct64_min;   // first t33: 64-octant
+  const bool oct64_6 = (L >> 9) / 64 >= (uint64_t)c->num_cus * c->t33_oct64_min;   // second t33: 64-octant
+  uint32_t d0t_order = c->mall_order && ns >= 2 && steps[0].kind == GS_D0T && steps[1].kind == GS_T33 &&
+                               ((L >> 3) / 32) % 16 == 0 && oct64_3 ? 1u : 0u;
+  if (d0t_order && c->mall_order >= 2 && ns >= 3 && steps[2].kind == GS_T33 && oct64_6 && ((L >> 6) / 64) % 8 == 0)
+    d0t_order = 2;
   std::vector<zk::RoundSink> sinks(nv);  // per round (a double uses its first round's, a tail one per round)
   std::vector<uint32_t> rtags(ns, 0);    // per step: the (first) challenge tag it waits for
   int inbuf = -1;                        // work buffer holding cur (-1: the input tables)
@@ -1084,7 +1095,8 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
       const uint64_t O = size / 8, nch = O / 32;
       const uint32_t res = grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F>) & ~1u;
       const uint32_t grid = step_grid(c, res, std::max<uint64_t>(2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax))) & ~1u;
-      launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, sk);
+      const uint32_t order = d0t_order;
+      launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, order, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
     }
@@ -1110,18 +1122,19 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
           const uint64_t nch = O / 64;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64>);
           const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
+          const uint32_t order = si == 1 ? d0t_order : 0u;  // (the pass right after an ordered k_gkr_d0t)
           if (c->t33_pipe)
             launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64, true>, grid, cur[0], cur[1], cur[2],
-                   cur[3], nx[0], nx[1], nx[2], nx[3], O, din, sk);
+                   cur[3], nx[0], nx[1], nx[2], nx[3], O, order, din, sk);
           else
             launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64>, grid, cur[0], cur[1], cur[2], cur[3],
-                   nx[0], nx[1], nx[2], nx[3], O, din, sk);
+                   nx[0], nx[1], nx[2], nx[3], O, order, din, sk);
         } else {
           const uint64_t nch = O / 32;
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 32>);
           const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<32> - 1) / zk::kT33ChunksMax<32>);
           launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 32>, grid, cur[0], cur[1], cur[2], cur[3],
-                 nx[0], nx[1], nx[2], nx[3], O, din, sk);
+                 nx[0], nx[1], nx[2], nx[3], O, 0u, din, sk);
         }
         for (int t = 0; t < 4; ++t) cur[t] = nx[t];
         enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);

@@ -716,10 +716,22 @@ __device__ __forceinline__ void d0t_flush(const i32x16 (&acc)[9], unsigned long 
   }
 }
 
+// order 2: the groups themselves in the order t33_group_perm, so that the
+// first k_gkr_t33 (reverse order) writes its LAST outputs as whole input sets
+// of the second k_gkr_t33's first chunks (64-octant both; ZK_MALL_ORDER=2)
+__device__ __forceinline__ uint64_t t33_group_perm(uint64_t j, uint64_t n3) {  // n3 = first-t33 chunks (8 | n3)
+  return (j >> 3) + (n3 >> 3) * (j & 7);
+}
+// order 1 (host.hpp, ZK_MALL_ORDER): logical chunk q is physical chunk
+// 2 g + (r & 1) + (r >> 1) nch / 8 with g = q / 16, r = q % 16 — the 16 chunks
+// of group g are exactly the inputs of the next step's (64-octant k_gkr_t33)
+// chunk g, so the pass's LAST reads are whole t33 chunks, which the next step
+// (order 1: chunks in reverse) reads FIRST, while the 256 MB Infinity Cache may
+// still hold them. Any order gives the same sums (exact integer tiles).
 template <class F>
 __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t O,
-                                                      RoundSink sink) {
+                                                      uint32_t order, RoundSink sink) {
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   __shared__ D0TScratch sc;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, half = l >> 5, ql = l & 31;
@@ -733,12 +745,20 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   const uint32_t pp = blockIdx.x & 1;
   const Fe* __restrict__ T = half ? (pp ? P : S) : (pp ? M : A);
   const uint64_t nch = O / 32, nb = gridDim.x >> 1;
+  auto phys = [&](uint64_t q) -> uint64_t {
+    if (!order) return q;
+    uint64_t g = q >> 4;
+    const uint64_t r = q & 15;
+    if (order == 2) g = t33_group_perm(g, nch >> 4);
+    return 2 * g + (r & 1) + (r >> 1) * (nch >> 3);
+  };
   uint64_t ch = blockIdx.x >> 1;
   Fe cn[2];
   if (ch < nch) {
-    ZK_DCHECK(ch * 32 + ql + (2 * w + 1) * O < 8 * O);
-    cn[0] = ld_fe(T, ch * 32 + ql + (2 * w) * O);
-    cn[1] = ld_fe(T, ch * 32 + ql + (2 * w + 1) * O);
+    const uint64_t pc = phys(ch);
+    ZK_DCHECK(pc * 32 + ql + (2 * w + 1) * O < 8 * O);
+    cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
+    cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
   }
   uint32_t buf = 0;
   for (; ch < nch; ch += nb, buf ^= 1) {
@@ -748,9 +768,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
       st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
     }
     if (ch + nb < nch) {  // the next chunk's corners, in flight during this chunk's products
-      ZK_DCHECK((ch + nb) * 32 + ql + (2 * w + 1) * O < 8 * O);
-      cn[0] = ld_fe(T, (ch + nb) * 32 + ql + (2 * w) * O);
-      cn[1] = ld_fe(T, (ch + nb) * 32 + ql + (2 * w + 1) * O);
+      const uint64_t pc = phys(ch + nb);
+      ZK_DCHECK(pc * 32 + ql + (2 * w + 1) * O < 8 * O);
+      cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
+      cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
     }
     __syncthreads();  // the image of this chunk is complete (double buffering: one barrier per chunk)
     d0t_mfmas(sc.img[buf], acc);
@@ -921,13 +942,21 @@ template <class F, int OCT, bool PIPE = false>
 __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
-                                                      Fe* __restrict__ P2, uint64_t O, DIn din, RoundSink sink) {
+                                                      Fe* __restrict__ P2, uint64_t O, uint32_t order, DIn din,
+                                                      RoundSink sink) {
   constexpr int NI = 8;  // inputs per output
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, ql = l & 31, hh = l >> 5;
   const Fe* __restrict__ X = uniform_ptr(w == 0 ? A : (w == 1 ? S : (w == 2 ? M : P)));
   Fe* __restrict__ X2 = w == 0 ? A2 : (w == 1 ? S2 : (w == 2 ? M2 : P2));
   const uint64_t nch = O / OCT, h8 = 8 * O;  // level-i tables hold 8 O elements
+  // order 1 (ZK_MALL_ORDER, the pass after an order-1 k_gkr_d0t): logical chunk
+  // ch is physical chunk nch - 1 - ch — the chunks the previous pass read last
+  // first; order 2: through t33_group_perm as the order-2 input pass
+  auto pch = [&](uint64_t ch) -> uint64_t {
+    if (!order) return ch;
+    return order == 2 ? t33_group_perm(nch - 1 - ch, nch) : nch - 1 - ch;
+  };
   // A fold of a chunk past the block's last one (the prefetch two folds
   // ahead) loads chunk 0 instead: the load stays unconditional (a conditional
   // load made hipcc drain every load at each chunk boundary) and every block's
@@ -938,7 +967,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   // spills and 11 SGPR spills, 512 vs 470 us for the first launch.)
   // OCT 32: fold f = corners 2f (lanes 0-31) and 2f + 1 (lanes 32-63) of octants ch*32 + ql
   auto in_at = [&](uint64_t ch, int f, Fe (&x)[NI]) {
-    ch = ch < nch ? ch : 0;
+    ch = pch(ch < nch ? ch : 0);
     const uint64_t e = ch * 32 + ql + (uint64_t)(2 * f + hh) * O;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
@@ -953,7 +982,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
   // every block: its poll would wait behind these loads (vmcnt is in order),
   // so it loads after the challenges arrive.
   auto unit_at = [&](uint64_t ch, int u, Fe (&x)[8]) {  // OCT 64: the eight inputs of fold u (corner u of octants ch*64 + l)
-    ch = ch < nch ? ch : 0;
+    ch = pch(ch < nch ? ch : 0);
     const uint64_t e = ch * 64 + l + (uint64_t)u * O;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1037,8 +1066,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       int64_t W[8];
       fold_words(a0, a1, W);
       const Fe z = dm_finish<F>(W, fe_zero<F>());
-      ZK_DCHECK(ch * 64 + l + (uint64_t)f * O < 8 * O);
-      st_fold(X2, ch * 64 + l + (uint64_t)f * O, z);
+      ZK_DCHECK(pch(ch) * 64 + l + (uint64_t)f * O < 8 * O);
+      st_fold(X2, pch(ch) * 64 + l + (uint64_t)f * O, z);
       dm_row<F>(img2[buf][f][w][l], z);
       if ((f & 1) && prev) products(buf ^ 1, f >> 1);  // the previous chunk's products, a quarter at a time
     }
@@ -1073,8 +1102,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       int64_t W[8];
       fold_words(a0, a1, W);
       const Fe z = dm_finish<F>(W, fe_zero<F>());
-      ZK_DCHECK(ch * 64 + l + (uint64_t)f * O < 8 * O);
-      st_fold(X2, ch * 64 + l + (uint64_t)f * O, z);
+      ZK_DCHECK(pch(ch) * 64 + l + (uint64_t)f * O < 8 * O);
+      st_fold(X2, pch(ch) * 64 + l + (uint64_t)f * O, z);
       dm_row<F>(img[f][w][l], z);
     }
     __syncthreads();  // this chunk's image is complete
@@ -1114,8 +1143,8 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       in_at(f < 3 ? ch : ch + gridDim.x, f < 3 ? f + 1 : 0, nx);
       const uint32_t corner = 2 * f + hh;
       const Fe z = dm3_fold<F>(x, wf);
-      ZK_DCHECK(ch * 32 + ql + (uint64_t)corner * O < 8 * O);
-      st_fold(X2, ch * 32 + ql + (uint64_t)corner * O, z);
+      ZK_DCHECK(pch(ch) * 32 + ql + (uint64_t)corner * O < 8 * O);
+      st_fold(X2, pch(ch) * 32 + ql + (uint64_t)corner * O, z);
       dm_row<F>(sc.img[buf][corner][w][ql], z);
     }
     __syncthreads();  // this chunk's image is complete (double buffering: one barrier per chunk)
