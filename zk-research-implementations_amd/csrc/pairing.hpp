@@ -28,6 +28,8 @@
 #include <cstdint>
 #include <vector>
 
+#include <array>
+
 #include "ec.hpp"
 
 namespace zk {
@@ -102,7 +104,11 @@ inline Fq12 fq12_mul(const Fq12& a, const Fq12& b) {  // Karatsuba over w^2 = v
   const Fq6 s = fq6_mul(fq6_add(a.c0, a.c1), fq6_add(b.c0, b.c1));
   return {fq6_add(t0, fq6_mul_v(t1)), fq6_sub(fq6_sub(s, t0), t1)};
 }
-inline Fq12 fq12_sqr(const Fq12& a) { return fq12_mul(a, a); }
+inline Fq12 fq12_sqr(const Fq12& a) {  // complex squaring: (a0 + a1 w)^2 = (a0^2 + v a1^2) + 2 a0 a1 w, 2 Fq6 products
+  const Fq6 ab = fq6_mul(a.c0, a.c1);
+  const Fq6 t = fq6_mul(fq6_add(a.c0, a.c1), fq6_add(a.c0, fq6_mul_v(a.c1)));  // a0^2 + v a1^2 + (1 + v) a0 a1
+  return {fq6_sub(fq6_sub(t, ab), fq6_mul_v(ab)), fq6_add(ab, ab)};
+}
 inline Fq12 fq12_conj(const Fq12& a) { return {a.c0, fq6_neg(a.c1)}; }  // a^(q^6)
 inline Fq12 fq12_inv(const Fq12& a) {  // (c0 - c1 w) / (c0^2 - v c1^2)
   const Fq6 t = fq6_inv(fq6_sub(fq6_mul(a.c0, a.c0), fq6_mul_v(fq6_mul(a.c1, a.c1))));
@@ -197,27 +203,94 @@ inline Big divmod(const Big& a, const Big& d, Big& rem) {
 }
 }  // namespace bigu
 
-// (q^6 + 1) / r, computed once
+// (q^4 - q^2 + 1) / r, computed once (the hard part; (q^6 + 1) = (q^2 + 1)(q^4 - q^2 + 1))
 inline const std::vector<uint32_t>& final_exp_hard() {
   static const std::vector<uint32_t> e = [] {
     bigu::Big q(Bls12_381Fq::P, Bls12_381Fq::P + 12);
     const bigu::Big q2 = bigu::mul(q, q);
-    bigu::Big q6 = bigu::mul(bigu::mul(q2, q2), q2);
-    bigu::add_small(q6, 1);
+    bigu::Big q4 = bigu::mul(q2, q2);
+    bigu::add_small(q4, 1);
+    bigu::sub_in(q4, q2);  // q^4 - q^2 + 1
     bigu::Big r(8);
     for (int i = 0; i < 8; ++i) r[i] = Bls12_381Fr::P[i];
     bigu::trim(r);
     bigu::Big rem;
-    bigu::Big out = bigu::divmod(q6, r, rem);
-    if (!rem.empty()) out.clear();  // r must divide q^6 + 1; an empty exponent makes every check fail
+    bigu::Big out = bigu::divmod(q4, r, rem);
+    if (!rem.empty()) out.clear();  // r must divide q^4 - q^2 + 1; an empty exponent makes every check fail
     return out;
   }();
   return e;
 }
 
+// Frobenius a -> a^q. In the w-power basis of Fq12 (w^2 = v, w^6 = xi), a =
+// sum_k c_k w^k with c_0..c_5 = a00, a10, a01, a11, a02, a12, and
+// (c w^k)^q = conj(c) w^k xi^(k (q - 1) / 6): conjugate each Fq2 coefficient
+// and scale it by gamma_k = xi^(k (q - 1) / 6) (q = 1 mod 6), computed once.
+inline Fq2 fq2_pow(const Fq2& a, const std::vector<uint32_t>& e) {
+  Fq2 r = fq2_one();
+  for (size_t i = e.size(); i-- > 0;)
+    for (int b = 31; b >= 0; --b) {
+      r = fq2_sqr(r);
+      if ((e[i] >> b) & 1u) r = fq2_mul(r, a);
+    }
+  return r;
+}
+inline const std::array<Fq2, 6>& frob_gamma() {
+  static const std::array<Fq2, 6> g = [] {
+    bigu::Big q(Bls12_381Fq::P, Bls12_381Fq::P + 12);
+    bigu::Big one{1};
+    bigu::sub_in(q, one);  // q - 1
+    bigu::Big six{6}, rem;
+    const bigu::Big e = bigu::divmod(q, six, rem);  // (q - 1) / 6, exact
+    const Fq2 xi = {fq_one(), fq_one()};             // 1 + u
+    const Fq2 g1 = fq2_pow(xi, e);
+    std::array<Fq2, 6> out;
+    out[0] = fq2_one();
+    for (int k = 1; k < 6; ++k) out[k] = fq2_mul(out[k - 1], g1);
+    return out;
+  }();
+  return g;
+}
+inline Fq12 fq12_frobenius(const Fq12& a) {
+  const std::array<Fq2, 6>& g = frob_gamma();
+  Fq12 r;
+  r.c0.c0 = fq2_mul(fq2_conj(a.c0.c0), g[0]);
+  r.c1.c0 = fq2_mul(fq2_conj(a.c1.c0), g[1]);
+  r.c0.c1 = fq2_mul(fq2_conj(a.c0.c1), g[2]);
+  r.c1.c1 = fq2_mul(fq2_conj(a.c1.c1), g[3]);
+  r.c0.c2 = fq2_mul(fq2_conj(a.c0.c2), g[4]);
+  r.c1.c2 = fq2_mul(fq2_conj(a.c1.c2), g[5]);
+  return r;
+}
+// a^e with fixed 4-bit windows (e LE u32 limbs)
+inline Fq12 fq12_pow_w4(const Fq12& a, const std::vector<uint32_t>& e) {
+  Fq12 tab[16];
+  tab[0] = fq12_one();
+  tab[1] = a;
+  for (int i = 2; i < 16; ++i) tab[i] = fq12_mul(tab[i - 1], a);
+  Fq12 r = fq12_one();
+  bool started = false;
+  for (size_t i = e.size(); i-- > 0;)
+    for (int sh = 28; sh >= 0; sh -= 4) {
+      const uint32_t d = (e[i] >> sh) & 15u;
+      if (started)
+        for (int k = 0; k < 4; ++k) r = fq12_sqr(r);
+      if (d) {
+        r = started ? fq12_mul(r, tab[d]) : tab[d];
+        started = true;
+      }
+    }
+  return r;
+}
+
+// f^((q^12 - 1) / r) = f^((q^6 - 1)(q^2 + 1) (q^4 - q^2 + 1) / r): the easy part
+// by a conjugation, an inversion and two Frobenius maps, the hard part by a
+// windowed power (round 6; the same value as the generic (q^6 + 1) / r power
+// it replaces, pinned by the oracle's pairing values in the CPU tests)
 inline Fq12 final_exponentiation(const Fq12& f) {
-  const Fq12 easy = fq12_mul(fq12_conj(f), fq12_inv(f));  // f^(q^6 - 1)
-  return fq12_pow(easy, final_exp_hard());
+  const Fq12 e1 = fq12_mul(fq12_conj(f), fq12_inv(f));          // f^(q^6 - 1)
+  const Fq12 e2 = fq12_mul(fq12_frobenius(fq12_frobenius(e1)), e1);  // ^(q^2 + 1)
+  return fq12_pow_w4(e2, final_exp_hard());
 }
 
 // ---- G2 (the twist, over Fq2) -------------------------------------------------
