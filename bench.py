@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fold", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-tables (PCIe-inclusive) prove")
+    ap.add_argument("--no-serving", action="store_true", help="skip the two-proofs-in-flight serving leg")
     ap.add_argument("--cpu-fast-nvars", type=int, default=24, help="size of the OpenMP CPU restatement run")
     ap.add_argument("--no-circuit", action="store_true", help="skip the full GKR circuit prove (SURVEY 8(f2))")
     ap.add_argument("--no-config5", action="store_true", help="skip BLS12-381 GKR + KZG commit (BASELINE config 5)")
@@ -314,6 +315,74 @@ def fold_bench(ctx, field: int, nvars: int = 20, reps: int = 10) -> dict:
         "achieved_GBs": gbs,
         "frac_of_hbm_peak": gbs / HBM_PEAK_GBS,
     }
+
+
+def serving_bench(field: int, tabs, n: int, ref_ch, streams: int = 2, per: int = 40) -> dict:
+    """Serving shape, never `value`: `streams` independent proofs in flight on
+    the one GPU — one host thread and one context (stream, pinned page,
+    workspaces) each, the same device-resident tables (read only), fresh
+    transcripts. One proof's tail (rounds 6-23, latency-bound) overlaps the
+    other's large passes. Aggregate proofs/s and per-proof latency; every proof
+    must equal the headline proof (tools/serve_streams.py sweeps the count)."""
+    import ctypes as C
+    import threading
+
+    import numpy as np
+
+    import zk_amd
+    from zk_amd._lib import check, lib
+    from zk_amd.elems import as_limbs, ptr
+
+    arr = (C.c_void_p * 4)(*[t.ptr.value for t in tabs])
+    zero = as_limbs([0])
+    ctxs = [zk_amd.Context(tabs[0].ctx.device) for _ in range(streams)]
+    lat = [[] for _ in range(streams)]
+    ok = [True] * streams
+
+    def prove(c, ch):
+        coeffs = np.zeros((n, 3, 4), np.uint64)
+        nco = np.zeros(n, np.uint8)
+        tr = zk_amd.Transcript(field)
+        check(lib().zk_dev_gkr_sumcheck_prove_sharded(c.h, field, arr, n, 0, ptr(zero), tr.h, ptr(coeffs), ptr(nco),
+                                                      ptr(ch)))
+
+    try:
+        for c in ctxs:
+            ch = np.zeros((n, 4), np.uint64)
+            for _ in range(3):
+                prove(c, ch)
+        barrier = threading.Barrier(streams + 1)
+
+        def run(i):
+            ch = np.zeros((n, 4), np.uint64)
+            barrier.wait()
+            for _ in range(per):
+                t0 = time.perf_counter()
+                prove(ctxs[i], ch)
+                lat[i].append(time.perf_counter() - t0)
+                ok[i] = ok[i] and np.array_equal(ch, ref_ch)
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(streams)]
+        for t in th:
+            t.start()
+        barrier.wait()
+        t0 = time.perf_counter()
+        for t in th:
+            t.join()
+        wall = time.perf_counter() - t0
+    finally:
+        for c in ctxs:
+            c.close()
+    alll = sorted(x for lt in lat for x in lt)
+    if not all(ok):
+        raise SystemExit("serving leg: a concurrent proof differs from the headline proof")
+    total = streams * per
+    return {"workload": f"{streams} independent {n}-var gkr_prove streams on one GPU (one context and host thread each, "
+                        "shared read-only tables)",
+            "proofs": total, "proofs_per_s": total / wall, "ms_per_proof_aggregate": wall * 1e3 / total,
+            "field_ops_per_s": 32.0 * ((1 << n) - 1) * total / wall,
+            "latency_ms_median": alll[len(alll) // 2] * 1e3, "latency_ms_p90": alll[int(len(alll) * 0.9)] * 1e3,
+            "same_proof_as_headline": True}
 
 
 def e2e_bench(ctx, field: int, tabs, n: int, reps: int = 3) -> dict:
@@ -1015,6 +1084,8 @@ def main() -> None:
             out["config4_26var"] = cfg4
         if peer_leg is not None:
             out["peer_reduce_leg"] = peer_leg
+        if not args.no_serving and world == 1:
+            out["serving_2_streams"] = serving_bench(field, tabs, n, first_challenges)
         if not args.no_e2e and world == 1:
             e2e = e2e_bench(ctx, field, tabs, n)
             e2e["same_proof_as_device_resident"] = bool(np.array_equal(e2e.pop("challenges"), ch))

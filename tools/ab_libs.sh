@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B: default library vs variants in abtest/ (ZK_LIB_PATH), alternating, 20 proofs each
 cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-config4 --no-events"
+B="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-config5 --no-config4 --no-events"
 for rep in ${REPS:-1 2 3 4 5}; do
   for lib in "" "$@"; do
     ZK_LIB_PATH=$lib timeout -k 10 120 $B > /tmp/o.json 2>/dev/null || exit 1

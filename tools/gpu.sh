@@ -27,7 +27,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-SIDE="--no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-plain"
+SIDE="--no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-config5 --no-plain"
 
 fail() { echo "step $1 failed (exit $2)"; tail -40 "$3"; exit 1; }
 
@@ -104,7 +104,7 @@ for step in "$@"; do
     profile)
       bash tools/profile_bench.sh "${arg:-r5}" || fail $step $? gpurun_out/prof_${arg:-r5}.err ;;
     kzg)
-      timeout -k 10 600 python bench.py --no-cpu-baseline --no-fold --no-e2e --no-circuit --no-plain --no-config4 --steps 5 --warmup 2 > gpurun_out/kzg.json 2> gpurun_out/kzg.err || fail $step $? gpurun_out/kzg.err
+      timeout -k 10 600 python bench.py --no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-plain --no-config4 --steps 5 --warmup 2 > gpurun_out/kzg.json 2> gpurun_out/kzg.err || fail $step $? gpurun_out/kzg.err
       summ gpurun_out/kzg.json ;;
     mb)
       prog=${arg%%:*}

@@ -2,7 +2,7 @@
 # A/B of environment knobs on the default bench workload (no events), alternating
 # usage: tools/knobs.sh "ENV=.. ENV2=.." "ENV=.." ...   ("-" = defaults)
 cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-config4 --no-events"
+B="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-config5 --no-config4 --no-events"
 for rep in 1 2; do
   for cfg in "$@"; do
     if [ "$cfg" = "-" ]; then e=""; else e="$cfg"; fi

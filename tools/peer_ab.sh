@@ -1,5 +1,5 @@
 set -o pipefail
-Q="--no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-plain --no-config4"
+Q="--no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-config5 --no-plain --no-config4"
 mkdir -p gpurun_out/pab
 for rep in 1 2; do
   for mode in plain rccl peer; do

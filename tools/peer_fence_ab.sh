@@ -8,7 +8,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-SIDE="--no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-plain --no-config4"
+SIDE="--no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-config5 --no-plain --no-config4"
 for rep in $(seq 1 ${REPS:-4}); do
   for lib in "" "$PWD/abtest/nofence.so"; do
     ZK_LIB_PATH=$lib timeout -k 10 180 python3 bench.py --force-rccl --reduce peer --steps 30 --warmup 5 $SIDE \

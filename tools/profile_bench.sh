@@ -8,7 +8,7 @@
 set -e
 TAG=${1:-r1}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-config4 --no-plain"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fold --no-e2e --no-serving --no-circuit --no-config5 --no-config4 --no-plain"
 # Per-round launches while profiling: a pre-enqueued round kernel's duration
 # includes its wait for the host-posted challenge, and the profiler slows the
 # host; the kernels' work is identical either way.

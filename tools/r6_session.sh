@@ -1,7 +1,13 @@
 set -o pipefail
-# round 6 session 10: the GPU parity files against the device bounds-check build; KZG verify timing
-bash tools/gpu.sh checks > gpurun_out/r6_checks.log 2>&1 || { tail -30 gpurun_out/r6_checks.log; exit 1; }
-tail -4 gpurun_out/r6_checks.log
-timeout -k 10 600 python bench.py --no-cpu-baseline --no-fold --no-e2e --no-plain --no-config4 --steps 5 --warmup 2 > gpurun_out/kzg10.json 2> gpurun_out/kzg10.err || { tail gpurun_out/kzg10.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('gpurun_out/kzg10.json')); k=d['config5_bls12_381']; print({x: k[x] for x in k if x.endswith('_ms') or 'verified' in x}); print(d.get('gkr_circuit_kzg'))"
+# round 6 session 11: replicated fan-in accumulators (ZK_ACCUM_REP) parity + A/B + traces
+timeout -k 10 600 python -u -m pytest tests/test_gpu_large.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "baseline_workload or grid_capped or gkr" > gpurun_out/s11_tests.log 2>&1 || { tail -30 gpurun_out/s11_tests.log; exit 1; }
+tail -1 gpurun_out/s11_tests.log
+ZK_ACCUM_REP=8 timeout -k 10 600 python -u -m pytest tests/test_gpu_large.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "baseline_workload or grid_capped or gkr" > gpurun_out/s11_tests8.log 2>&1 || { tail -30 gpurun_out/s11_tests8.log; exit 1; }
+tail -1 gpurun_out/s11_tests8.log
+REPS=6 bash tools/gpu.sh abenv=-/ZK_ACCUM_REP=8/ZK_ACCUM_REP=16 > gpurun_out/rep_ab.log 2>&1 || { tail gpurun_out/rep_ab.log; exit 1; }
+cat gpurun_out/rep_ab.log
+for rep in 1 8; do
+  ZK_ACCUM_REP=$rep ZK_DEBUG_TAIL=1 timeout -k 10 120 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fold --no-e2e --no-circuit --no-config5 --no-plain --no-config4 --no-events > /tmp/t.json 2> /tmp/t.err || exit 1
+  echo "== ZK_ACCUM_REP=$rep"; grep "zk step\|zk dtail" /tmp/t.err | tail -8
+done > gpurun_out/rep_trace.log
+cat gpurun_out/rep_trace.log
