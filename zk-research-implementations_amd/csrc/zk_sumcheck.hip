@@ -673,7 +673,12 @@ int zk_ctx_attach_peer_reduce(zk_ctx* c, int enable, int* out_ok) {
     if (!enable) return;
     require(c->comm != COMM_NONE, "attach a communicator first");
     require(c->world <= (int)zk::kPeerMax, "peer reduction joins at most 8 ranks (one node)");
-    peer_attach(c);
+    try {
+      peer_attach(c);
+    } catch (...) {  // (e.g. the communicator failed mid-attach: nothing half-attached stays behind)
+      peer_release(c);
+      throw;
+    }
     if (out_ok) *out_ok = 1;
   });
 }
