@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x)                                                                   \
@@ -87,6 +88,80 @@ __global__ __launch_bounds__(256, 1) void k_order(Tabs t, size_t O) {
   }
 }
 
+// longer runs: each lane folds RUN consecutive outputs per fold (the wave's
+// runs are 2 RUN KiB per input and output), chunks of 64 RUN octants, the
+// kernel's chunk order, AHEAD folds of loads in flight
+template <int RUN, int AHEAD>
+__global__ __launch_bounds__(256, 1) void k_runs(Tabs t, size_t O) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* __restrict__ X = t.in[w];
+  uint4* __restrict__ X2 = t.out[w];
+  const size_t OCT = 64 * RUN, nch = O / OCT, h8 = 8 * O, G = gridDim.x;
+  const size_t cpb = (nch + G - 1) / G;
+  constexpr int NS = AHEAD + 1;
+  uint4 a[NS][8][RUN], b[NS][8][RUN];
+  const size_t units = cpb * 8;
+  auto base = [&](size_t u) -> size_t {  // first output of lane l in unit u (clamped like the kernel)
+    size_t ch = blockIdx.x + (u / 8) * G;
+    if (ch >= nch) ch = 0;
+    return ch * OCT + (size_t)l * RUN + (size_t)(u % 8) * O;
+  };
+  auto load = [&](size_t u, int s) {
+    const size_t e = base(u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int q = 0; q < RUN; ++q) {
+        a[s][k][q] = X[2 * (e + q + k * h8)];
+        b[s][k][q] = X[2 * (e + q + k * h8) + 1];
+      }
+  };
+#pragma unroll
+  for (int s = 0; s < AHEAD; ++s) load(s, s);
+  for (size_t u0 = 0; u0 < units; u0 += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const size_t u = u0 + s;
+      if (AHEAD) load(u + AHEAD, (s + AHEAD) % NS); else load(u, s);
+      if (u < units && blockIdx.x + (u / 8) * G < nch) {
+        const size_t e = base(u);
+#pragma unroll
+        for (int q = 0; q < RUN; ++q) {
+          uint4 x = a[s][0][q], y = b[s][0][q];
+#pragma unroll
+          for (int k = 1; k < 8; ++k) {
+            xr(x, a[s][k][q]);
+            xr(y, b[s][k][q]);
+          }
+          X2[2 * (e + q)] = x;
+          X2[2 * (e + q) + 1] = y;
+        }
+      }
+    }
+  }
+}
+template <int RUN, int AHEAD>
+float run_runs(const Tabs& t, size_t O, int grid, int reps) {
+  if (O % (64 * RUN)) exit(1);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> v;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_runs<RUN, AHEAD>), dim3(grid), dim3(256), 0, 0, t, O);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    v.push_back(ms * 1000.f);
+  }
+  std::sort(v.begin(), v.end());
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return v[v.size() / 2];
+}
+
 template <int ORDER, int AHEAD, bool ST>
 float run(const Tabs& t, size_t O, int grid, int reps) {
   const size_t nch = O / 64;
@@ -126,6 +201,20 @@ int main() {
   const size_t O = N / 64;  // 2^18 octants
   const double rd = 4.0 * N * 32, wr = 4.0 * N / 8 * 32;
   const int reps = 9;
+  if (getenv("MB_RUNS")) {  // round 6: run length (2 / 4 / 8 KiB per input and output run)
+    for (int pass = 0; pass < 2; ++pass)
+      for (int grid : {256, 512}) {
+        const float r1a1 = run_runs<1, 1>(t, O, grid, reps), r1a2 = run_runs<1, 2>(t, O, grid, reps);
+        const float r2a1 = run_runs<2, 1>(t, O, grid, reps), r2a0 = run_runs<2, 0>(t, O, grid, reps);
+        const float r4a0 = run_runs<4, 0>(t, O, grid, reps);
+        auto tb = [&](float us) { return (rd + wr) / us / 1e6; };
+        printf("grid %d W8 runs: 2 KiB %6.1f us (%.2f TB/s) / 2 ahead %6.1f (%.2f) | 4 KiB %6.1f (%.2f) / no prefetch "
+               "%6.1f (%.2f) | 8 KiB (no prefetch) %6.1f (%.2f)\n",
+               grid, r1a1, tb(r1a1), r1a2, tb(r1a2), r2a1, tb(r2a1), r2a0, tb(r2a0), r4a0, tb(r4a0));
+        fflush(stdout);
+      }
+    return 0;
+  }
   for (int pass = 0; pass < 2; ++pass) {
     for (int grid : {256, 512}) {
       const float s1 = run<STRIDE, 1, true>(t, O, grid, reps), s2 = run<STRIDE, 2, true>(t, O, grid, reps);
