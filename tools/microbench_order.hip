@@ -162,6 +162,69 @@ float run_runs(const Tabs& t, size_t O, int grid, int reps) {
   return v[v.size() / 2];
 }
 
+// an octant-major input layout (the eight corners of an output adjacent: its
+// 256 B at 8 e): a wave reads one contiguous 16 KiB run per 64 outputs (16
+// lane-contiguous uint4 loads) and writes their 2 KiB run — the same bytes as
+// k_order in one read stream and one write stream; AHEAD units of loads in flight
+template <int AHEAD>
+__global__ __launch_bounds__(256, 1) void k_seq(Tabs t, size_t nout) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint4* __restrict__ X = t.in[w];
+  uint4* __restrict__ X2 = t.out[w];
+  const size_t nch = nout / 64, G = gridDim.x, units = (nch + G - 1) / G;
+  constexpr int NS = AHEAD + 1;
+  uint4 a[NS][16];
+  auto chunk = [&](size_t u) -> size_t {
+    const size_t ch = blockIdx.x + u * G;
+    return ch < nch ? ch : 0;
+  };
+  auto load = [&](size_t u, int s) {
+    const uint4* p = X + chunk(u) * 1024 + l;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[s][j] = p[j * 64];
+  };
+#pragma unroll
+  for (int s = 0; s < AHEAD; ++s) load(s, s);
+  for (size_t u0 = 0; u0 < units; u0 += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const size_t u = u0 + s;
+      if (AHEAD) load(u + AHEAD, (s + AHEAD) % NS); else load(u, s);
+      if (u < units && blockIdx.x + u * G < nch) {
+        uint4 x = a[s][0], y = a[s][1];
+#pragma unroll
+        for (int j = 2; j < 16; j += 2) {
+          xr(x, a[s][j]);
+          xr(y, a[s][j + 1]);
+        }
+        const size_t e = (blockIdx.x + u * G) * 64 + l;
+        X2[2 * e] = x;
+        X2[2 * e + 1] = y;
+      }
+    }
+  }
+}
+template <int AHEAD>
+float run_seq(const Tabs& t, size_t nout, int grid, int reps) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> v;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((k_seq<AHEAD>), dim3(grid), dim3(256), 0, 0, t, nout);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    v.push_back(ms * 1000.f);
+  }
+  std::sort(v.begin(), v.end());
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return v[v.size() / 2];
+}
+
 template <int ORDER, int AHEAD, bool ST>
 float run(const Tabs& t, size_t O, int grid, int reps) {
   const size_t nch = O / 64;
@@ -201,6 +264,20 @@ int main() {
   const size_t O = N / 64;  // 2^18 octants
   const double rd = 4.0 * N * 32, wr = 4.0 * N / 8 * 32;
   const int reps = 9;
+  if (getenv("MB_SEQ")) {  // round 6: octant-major inputs against the kernel's layout
+    for (int pass = 0; pass < 3; ++pass)
+      for (int grid : {256, 512, 1024}) {
+        const float k2 = run<STRIDE, 2, true>(t, O, grid, reps);
+        const float q1 = run_seq<1>(t, N / 8, grid, reps), q2 = run_seq<2>(t, N / 8, grid, reps);
+        const float q0 = run_seq<0>(t, N / 8, grid, reps);
+        auto tb = [&](float us) { return (rd + wr) / us / 1e6; };
+        printf("grid %4d: kernel layout (8 x 2 KiB runs, 2 ahead) %6.1f us (%.2f TB/s) | octant-major 1 ahead %6.1f (%.2f) "
+               "2 ahead %6.1f (%.2f) none %6.1f (%.2f)\n",
+               grid, k2, tb(k2), q1, tb(q1), q2, tb(q2), q0, tb(q0));
+        fflush(stdout);
+      }
+    return 0;
+  }
   if (getenv("MB_RUNS")) {  // round 6: run length (2 / 4 / 8 KiB per input and output run)
     for (int pass = 0; pass < 2; ++pass)
       for (int grid : {256, 512}) {
