@@ -32,6 +32,11 @@ struct Tabs {
   const uint4* in[4];
   uint4* out[4];
 };
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void xr(uint4& a, const uint4& c) {
   a.x ^= c.x;
   a.y ^= c.y;
@@ -40,7 +45,7 @@ __device__ __forceinline__ void xr(uint4& a, const uint4& c) {
 }
 
 // O: octants of the output level; the 8 inputs of output e are e + k 8 O
-template <int ORDER, int AHEAD, bool ST>
+template <int ORDER, int AHEAD, bool ST, bool LNT = false>
 __global__ __launch_bounds__(256, 1) void k_order(Tabs t, size_t O) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const uint4* __restrict__ X = t.in[w];
@@ -58,8 +63,13 @@ __global__ __launch_bounds__(256, 1) void k_order(Tabs t, size_t O) {
     const size_t e = chunk(uu / 8) * 64 + l + (size_t)((f0 + uu % 8) & 7) * O;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      a[s][k] = X[2 * (e + k * h8)];
-      b[s][k] = X[2 * (e + k * h8) + 1];
+      if (LNT) {  // non-temporal loads (MB_MALL)
+        a[s][k] = ld_nt(&X[2 * (e + k * h8)]);
+        b[s][k] = ld_nt(&X[2 * (e + k * h8) + 1]);
+      } else {
+        a[s][k] = X[2 * (e + k * h8)];
+        b[s][k] = X[2 * (e + k * h8) + 1];
+      }
     }
   };
 #pragma unroll
@@ -225,6 +235,34 @@ float run_seq(const Tabs& t, size_t nout, int grid, int reps) {
   return v[v.size() / 2];
 }
 
+// MB_MALL: does the second fold pass find the first one's outputs in the
+// Infinity Cache? W8 over the inputs (plain or non-temporal loads) writes the
+// 268 MB level; then the same pattern one level down (O / 8) reads it back,
+// timed alone. 'cold': the read-back after a read-only stream of the inputs.
+template <bool LNT>
+void mall_pair(const Tabs& t, const Tabs& t2, size_t O, int grid, float& first, float& second, bool cold) {
+  hipEvent_t e0, e1, e2;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventCreate(&e2));
+  CK(hipEventRecord(e0));
+  if (cold)
+    hipLaunchKernelGGL((k_order<STRIDE, 2, false, false>), dim3(grid), dim3(256), 0, 0, t, O);
+  else
+    hipLaunchKernelGGL((k_order<STRIDE, 2, true, LNT>), dim3(grid), dim3(256), 0, 0, t, O);
+  CK(hipEventRecord(e1));
+  hipLaunchKernelGGL((k_order<STRIDE, 2, true, false>), dim3(256), dim3(256), 0, 0, t2, O / 8);
+  CK(hipEventRecord(e2));
+  CK(hipEventSynchronize(e2));
+  CK(hipEventElapsedTime(&first, e0, e1));
+  CK(hipEventElapsedTime(&second, e1, e2));
+  first *= 1000.f;
+  second *= 1000.f;
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  CK(hipEventDestroy(e2));
+}
+
 template <int ORDER, int AHEAD, bool ST>
 float run(const Tabs& t, size_t O, int grid, int reps) {
   const size_t nch = O / 64;
@@ -264,6 +302,25 @@ int main() {
   const size_t O = N / 64;  // 2^18 octants
   const double rd = 4.0 * N * 32, wr = 4.0 * N / 8 * 32;
   const int reps = 9;
+  if (getenv("MB_MALL")) {
+    Tabs t2;
+    for (int i = 0; i < 4; ++i) {
+      t2.in[i] = t.out[i];
+      CK(hipMalloc(&t2.out[i], N / 64 * 32));
+    }
+    const double rb = 4.0 * N / 8 * 32 + 4.0 * N / 64 * 32;
+    for (int pass = 0; pass < 8; ++pass) {
+      float f0, s0, f1, s1, f2, s2;
+      mall_pair<false>(t, t2, O, 256, f0, s0, false);
+      mall_pair<true>(t, t2, O, 256, f1, s1, false);
+      mall_pair<false>(t, t2, O, 256, f2, s2, true);
+      printf("W8 plain loads %6.1f us -> read-back %5.1f us (%.2f TB/s) | W8 nt loads %6.1f -> read-back %5.1f (%.2f) | "
+             "after a read-only stream (cold) %5.1f (%.2f)\n",
+             f0, s0, rb / s0 / 1e6, f1, s1, rb / s1 / 1e6, s2, rb / s2 / 1e6);
+      fflush(stdout);
+    }
+    return 0;
+  }
   if (getenv("MB_SEQ")) {  // round 6: octant-major inputs against the kernel's layout
     for (int pass = 0; pass < 3; ++pass)
       for (int grid : {256, 512, 1024}) {
