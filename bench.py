@@ -966,8 +966,10 @@ def main() -> None:
     import re
 
     # the newest round's PMC traffic file (profiles/r<N>_traffic.json, tools/pmc_traffic.py)
-    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")),
-                    key=lambda f: int(re.match(r"r(\d+)_", os.path.basename(f)).group(1)))
+    # (r6f_traffic.json: round 6's last tree, after r6_traffic.json)
+    tfiles = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json"))
+                     if re.match(r"r\d+[a-z]*_traffic\.json$", os.path.basename(f))),
+                    key=lambda f: (int(re.match(r"r(\d+)", os.path.basename(f)).group(1)), os.path.basename(f)))
     tpath = tfiles[-1] if tfiles else ""
     if os.path.exists(tpath) and n == 24:
         t = json.load(open(tpath))
