@@ -1605,6 +1605,9 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
               m, (T[m * 8 + 1] - T[m * 8]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 3] - T[m * 8 + 2]) * 0.01,
               (T[m * 8 + 4] - T[m * 8 + 3]) * 0.01, (T[m * 8 + 5] - T[m * 8 + 4]) * 0.01,
               m + 1 < nd ? (T[m * 8 + 9] - T[m * 8 + 5]) * 0.01 : 0.0);
+    for (uint32_t m = 0; m < nd; ++m)  // block 0's fold+eval: constants, loop, store drain
+      fprintf(stderr, "zk dtail step %u fold+eval: constants %6.2f us, loop %6.2f, store drain %6.2f\n", m,
+              (T[m * 8 + 6] - T[m * 8 + 1]) * 0.01, (T[m * 8 + 7] - T[m * 8 + 6]) * 0.01, (T[m * 8 + 2] - T[m * 8 + 7]) * 0.01);
   }
 }
 

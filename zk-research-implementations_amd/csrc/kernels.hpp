@@ -1254,6 +1254,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 1] = __builtin_amdgcn_s_memrealtime();
     const bool two = st > 0 || a.np0 == 2;
     fold_consts<F, 3>(ra, rb, rab, ct);  // blocks 0, 1, 2: ra, rb, ra rb
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 6] = __builtin_amdgcn_s_memrealtime();
     const uint64_t h4 = 4 * Q;
     const Fe* X;
     if (st == 0) {
@@ -1278,6 +1279,7 @@ __global__ __launch_bounds__(kBlock) void k_gkr_dtail(DTailArgs a, RoundSink sin
         unit_product<F>(z, k, tab, acc);
       }
     }
+    if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 7] = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's table stores have landed
     if (a.trace && blockIdx.x == 0 && threadIdx.x == 0) a.trace[st * 8 + 2] = __builtin_amdgcn_s_memrealtime();
     dround_limb_sums(acc, sc);
