@@ -263,7 +263,7 @@ void mall_pair(const Tabs& t, const Tabs& t2, size_t O, int grid, float& first, 
   CK(hipEventDestroy(e2));
 }
 
-template <int ORDER, int AHEAD, bool ST>
+template <int ORDER, int AHEAD, bool ST, bool LNT = false>
 float run(const Tabs& t, size_t O, int grid, int reps) {
   const size_t nch = O / 64;
   if (O % 64 || nch % grid || 8 * O * 8 > (1ull << 24)) {
@@ -276,7 +276,7 @@ float run(const Tabs& t, size_t O, int grid, int reps) {
   std::vector<float> v;
   for (int r = 0; r < reps; ++r) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_order<ORDER, AHEAD, ST>), dim3(grid), dim3(256), 0, 0, t, O);
+    hipLaunchKernelGGL((k_order<ORDER, AHEAD, ST, LNT>), dim3(grid), dim3(256), 0, 0, t, O);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -302,6 +302,18 @@ int main() {
   const size_t O = N / 64;  // 2^18 octants
   const double rd = 4.0 * N * 32, wr = 4.0 * N / 8 * 32;
   const int reps = 9;
+  if (getenv("MB_RNT")) {  // round 6: the read-only pattern (k_gkr_d0t's shape) with non-temporal loads
+    for (int pass = 0; pass < 3; ++pass)
+      for (int grid : {256, 512, 1024}) {
+        const float p1 = run<STRIDE, 1, false, false>(t, O, grid, reps), n1 = run<STRIDE, 1, false, true>(t, O, grid, reps);
+        const float p2 = run<STRIDE, 2, false, false>(t, O, grid, reps), n2 = run<STRIDE, 2, false, true>(t, O, grid, reps);
+        auto tb = [&](float us) { return rd / us / 1e6; };
+        printf("grid %4d R8: plain 1 ahead %6.1f us (%.2f TB/s) nt %6.1f (%.2f) | plain 2 ahead %6.1f (%.2f) nt %6.1f (%.2f)\n",
+               grid, p1, tb(p1), n1, tb(n1), p2, tb(p2), n2, tb(n2));
+        fflush(stdout);
+      }
+    return 0;
+  }
   if (getenv("MB_MALL")) {
     Tabs t2;
     for (int i = 0; i < 4; ++i) {

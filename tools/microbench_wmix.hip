@@ -42,6 +42,11 @@ __device__ __forceinline__ void nt_store(uint4* p, const uint4& v) {
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
 }
 
+typedef uint32_t v4u_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+  const v4u_nt v = __builtin_nontemporal_load(reinterpret_cast<const v4u_nt*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ void xr(uint4& a, const uint4& c) {
   a.x ^= c.x;
   a.y ^= c.y;
@@ -130,7 +135,7 @@ float run(const Tabs& t, size_t O, int grid, int reps) {
 // RUN (round 5): each wave writes its chunk's NF folds as ONE contiguous run
 // (output index (ch NF + f) 64 + l: 16 KiB per chunk and table) instead of NF
 // runs of 2 KiB spread over the level-3 table; NTS: non-temporal stores
-template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false, bool RUN = false, bool NTS = false>
+template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false, bool RUN = false, bool NTS = false, bool NTL = false>
 __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const uint4* __restrict__ X = t.in[w];
@@ -141,7 +146,14 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
     const size_t e = ch * 64 + l + (size_t)f * O;
 #pragma unroll
     for (int k = 0; k < NIN; ++k) {
-      if (LDC) {
+      if (LDC && NTL) {  // (round 6: non-temporal, whole lines per instruction)
+        const size_t r = ch * 64 + (size_t)f * O + k * hs;
+        na[k] = ld_nt(&X[2 * r + l]);
+        nb[k] = ld_nt(&X[2 * r + 64 + l]);
+      } else if (NTL) {
+        na[k] = ld_nt(&X[2 * (e + k * hs)]);
+        nb[k] = ld_nt(&X[2 * (e + k * hs) + 1]);
+      } else if (LDC) {
         const size_t r = ch * 64 + (size_t)f * O + k * hs;  // the run's first element
         na[k] = X[2 * r + l];
         nb[k] = X[2 * r + 64 + l];
@@ -187,7 +199,7 @@ __global__ __launch_bounds__(256, 1) void k_mix_pf(Tabs t, size_t O) {
   }
 }
 
-template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false, bool RUN = false, bool NTS = false>
+template <int NIN, int NF, bool ST, bool LDC = false, bool STC = false, bool RUN = false, bool NTS = false, bool NTL = false>
 float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   const size_t in_max = (O - 1) + (size_t)(NF - 1) * O + (size_t)(NIN - 1) * NF * O, out_max = NF * O - 1;
   if (O % 64 || in_max >= (1ull << 24) || out_max >= (1ull << 24) / 8) {
@@ -200,7 +212,7 @@ float run_pf(const Tabs& t, size_t O, int grid, int reps) {
   std::vector<float> v;
   for (int r = 0; r < reps; ++r) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_mix_pf<NIN, NF, ST, LDC, STC, RUN, NTS>), dim3(grid), dim3(256), 0, 0, t, O);
+    hipLaunchKernelGGL((k_mix_pf<NIN, NF, ST, LDC, STC, RUN, NTS, NTL>), dim3(grid), dim3(256), 0, 0, t, O);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -224,7 +236,7 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-template <int NF, bool ST, int KU, int DEPTH, int WPS>
+template <int NF, bool ST, int KU, int DEPTH, int WPS, int AUX = 0>
 __global__ __launch_bounds__(256, WPS) void k_mix_glds(Tabs t, size_t O) {
   constexpr int NIN = 8, UPF = NIN / KU;  // units per fold
   __shared__ uint4 ring[4][DEPTH][KU][128];
@@ -243,8 +255,8 @@ __global__ __launch_bounds__(256, WPS) void k_mix_glds(Tabs t, size_t O) {
     for (int k = 0; k < KU; ++k) {
       const char* g = (const char*)(X + 2 * (e0 + (size_t)(h * KU + k) * hs)) + 16 * l;
       __attribute__((address_space(3))) void* d = (__attribute__((address_space(3))) void*)&ring[w][u % DEPTH][k][0];
-      __builtin_amdgcn_global_load_lds((const void*)g, d, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(g + 1024), (__attribute__((address_space(3))) void*)&ring[w][u % DEPTH][k][64], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)g, d, 16, 0, AUX);
+      __builtin_amdgcn_global_load_lds((const void*)(g + 1024), (__attribute__((address_space(3))) void*)&ring[w][u % DEPTH][k][64], 16, 0, AUX);
     }
   };
   if (nu == 0) return;
@@ -276,7 +288,7 @@ __global__ __launch_bounds__(256, WPS) void k_mix_glds(Tabs t, size_t O) {
   wait_vm<0>();
 }
 
-template <int NF, bool ST, int KU, int DEPTH, int WPS>
+template <int NF, bool ST, int KU, int DEPTH, int WPS, int AUX = 0>
 float run_glds(const Tabs& t, size_t O, int grid, int reps) {
   const size_t in_max = (O - 1) + (size_t)(NF - 1) * O + (size_t)7 * NF * O, out_max = NF * O - 1;
   if (O % 64 || in_max >= (1ull << 24) || out_max >= (1ull << 24) / 8) {
@@ -289,7 +301,7 @@ float run_glds(const Tabs& t, size_t O, int grid, int reps) {
   std::vector<float> v;
   for (int r = 0; r < reps; ++r) {
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((k_mix_glds<NF, ST, KU, DEPTH, WPS>), dim3(grid), dim3(256), 0, 0, t, O);
+    hipLaunchKernelGGL((k_mix_glds<NF, ST, KU, DEPTH, WPS, AUX>), dim3(grid), dim3(256), 0, 0, t, O);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
@@ -409,6 +421,40 @@ int main(int argc, char** argv) {
   }
   const double rd = 4.0 * N * 32;
   const int reps = 7;
+  if (argc > 1 && std::string(argv[1]) == "pfnt") {  // round 6: register loads, nt, element vs lane-contiguous shape
+    const size_t O8 = N / 64;
+    const double wr8 = 4.0 * N / 8 * 32;
+    for (int pass = 0; pass < 3; ++pass)
+      for (int grid : {256, 512}) {
+        const float re = run_pf<8, 8, false>(t, O8, grid, reps), ren = run_pf<8, 8, false, false, false, false, false, true>(t, O8, grid, reps);
+        const float rl = run_pf<8, 8, false, true>(t, O8, grid, reps), rln = run_pf<8, 8, false, true, false, false, false, true>(t, O8, grid, reps);
+        const float we = run_pf<8, 8, true>(t, O8, grid, reps), wen = run_pf<8, 8, true, false, false, false, false, true>(t, O8, grid, reps);
+        const float wl = run_pf<8, 8, true, true>(t, O8, grid, reps), wln = run_pf<8, 8, true, true, false, false, false, true>(t, O8, grid, reps);
+        auto r_ = [&](float us) { return rd / us / 1e6; };
+        auto w_ = [&](float us) { return (rd + wr8) / us / 1e6; };
+        printf("regs grid %4d: R8 elem %6.1f (%.2f) nt %6.1f (%.2f) | R8 lane-contig %6.1f (%.2f) nt %6.1f (%.2f) | W8 elem %6.1f (%.2f) "
+               "nt %6.1f (%.2f) | W8 lane-contig %6.1f (%.2f) nt %6.1f (%.2f)\n",
+               grid, re, r_(re), ren, r_(ren), rl, r_(rl), rln, r_(rln), we, w_(we), wen, w_(wen), wl, w_(wl), wln, w_(wln));
+        fflush(stdout);
+      }
+    return 0;
+  }
+  if (argc > 1 && std::string(argv[1]) == "gldsnt") {  // round 6: LDS-DMA with the non-temporal policy (aux 2)
+    const size_t O8 = N / 64;
+    const double wr8 = 4.0 * N / 8 * 32;
+    for (int pass = 0; pass < 3; ++pass)
+      for (int grid : {256, 512, 1024}) {
+        const float r1 = run_glds<8, false, 8, 2, 1>(t, O8, grid, reps), r1n = run_glds<8, false, 8, 2, 1, 2>(t, O8, grid, reps);
+        const float r2 = run_glds<8, false, 4, 2, 2>(t, O8, grid, reps), r2n = run_glds<8, false, 4, 2, 2, 2>(t, O8, grid, reps);
+        const float w1 = run_glds<8, true, 8, 2, 1>(t, O8, grid, reps), w1n = run_glds<8, true, 8, 2, 1, 2>(t, O8, grid, reps);
+        printf("LDS-DMA grid %4d: R8 1 w/SIMD %6.1f us (%.2f TB/s) nt %6.1f (%.2f) | R8 2 w/SIMD %6.1f (%.2f) nt %6.1f (%.2f) | "
+               "W8 1 w/SIMD %6.1f (%.2f) nt loads %6.1f (%.2f)\n",
+               grid, r1, rd / r1 / 1e6, r1n, rd / r1n / 1e6, r2, rd / r2 / 1e6, r2n, rd / r2n / 1e6, w1, (rd + wr8) / w1 / 1e6,
+               w1n, (rd + wr8) / w1n / 1e6);
+        fflush(stdout);
+      }
+    return 0;
+  }
   {  // calibration: copy 4 x 256 MiB (the output buffers hold N/8 elements: copy that much)
     const size_t n4 = N / 8 * 2;
     hipEvent_t e0, e1;

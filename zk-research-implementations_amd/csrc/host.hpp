@@ -224,6 +224,9 @@ struct zk_ctx {
   uint32_t gather_vars = 10;  // sharded: gather the tables once <= this many local rounds remain, finish locally (ZK_GATHER_VARS; 0: at the end)
   DevBuf gbuf;                // sharded gather: fold scratch, the one-hot buffer, the interleaved global tables
   bool t33_pipe = true;  // ZK_T33_PIPE (0: off): the 64-octant k_gkr_t33 with a double-buffered image, products interleaved
+  // ZK_LC_LOADS: lane-contiguous non-temporal input loads (mfma.hpp ld_half_nt) —
+  // bit 0 k_gkr_d0t, bit 1 the first k_gkr_t33 (over the input tables), bit 2 the later 64-octant ones
+  uint32_t lc_loads = 7;
   uint32_t mall_order = 0;  // ZK_MALL_ORDER: k_gkr_d0t reads the first k_gkr_t33's chunks grouped, that t33 walks them in reverse; 2: the groups permuted for the second t33 too (mfma.hpp)
   uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks; round 6: 4 -> 1, the second pass 2 us faster, profiles/r6_knob_ab.txt)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
@@ -1093,10 +1096,14 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
     }
     if (st.kind == GS_D0T) {  // rounds 0, 1, 2 over the input tables (size 8 O), nothing written
       const uint64_t O = size / 8, nch = O / 32;
-      const uint32_t res = grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F>) & ~1u;
+      const uint32_t res = ((c->lc_loads & 1u) ? grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F, true>)
+                                                : grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F>)) & ~1u;
       const uint32_t grid = step_grid(c, res, std::max<uint64_t>(2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax))) & ~1u;
       const uint32_t order = d0t_order;
-      launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, order, sk);
+      if (c->lc_loads & 1u)
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F, true>, grid, cur[0], cur[1], cur[2], cur[3], O, order, sk);
+      else
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, order, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
     }
@@ -1123,7 +1130,11 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
           const uint32_t res = grid_for(c, nch * zk::kBlock, zk::k_gkr_t33<F, 64>);
           const uint32_t grid = step_grid(c, res, (nch + zk::kT33ChunksMax<64> - 1) / zk::kT33ChunksMax<64>);
           const uint32_t order = si == 1 ? d0t_order : 0u;  // (the pass right after an ordered k_gkr_d0t)
-          if (c->t33_pipe)
+          const bool lc = c->t33_pipe && (c->lc_loads & (si == 1 ? 2u : 4u));
+          if (lc)
+            launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64, true, true>, grid, cur[0], cur[1], cur[2],
+                   cur[3], nx[0], nx[1], nx[2], nx[3], O, order, din, sk);
+          else if (c->t33_pipe)
             launch(c, ZK_K_GKR_T33, 9216.0 * O, 96.0 * O, zk::k_gkr_t33<F, 64, true>, grid, cur[0], cur[1], cur[2],
                    cur[3], nx[0], nx[1], nx[2], nx[3], O, order, din, sk);
           else

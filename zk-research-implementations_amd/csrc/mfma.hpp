@@ -303,6 +303,55 @@ __device__ __forceinline__ void fold_operands(const Fe& x, i32x4& b0, i32x4& b1)
     b1[q] = (int)r[1];
   }
 }
+// Lane-contiguous non-temporal input loads (round 6, ZK_LC_LOADS). A wave's
+// 64 lanes load the 1 KiB of 32 consecutive elements e0 .. e0 + 31 as whole
+// 128-B lines: lane l takes bytes 16 (l >> 5) .. +15 of element e0 + (l & 31).
+// That is a fold MFMA's B operand as it stands ([digits 0-15 of elements
+// 0-31 | digits 16-31 of the same], fold_operands), and a digit-image row half
+// for the round-sum images. Measured memory-only (tools/microbench_wmix.hip
+// pfnt / gldsnt): the element-per-lane shape (two 16-B loads per lane, each
+// instruction touching half of every line) streams 2 GiB at 6.3 TB/s with the
+// default policy and 5.6 with nt; whole lines per instruction with nt, 7.1 TB/s
+// (the first fold pass's read/write mix: 481 -> 445 us).
+__device__ __forceinline__ u32x4 ld_half_nt(const Fe* __restrict__ X, uint64_t e0) {
+  const uint32_t l = threadIdx.x & 63;
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X) + 2 * (e0 + (l & 31)) + (l >> 5));
+}
+// digits (to_digits) of N values held as ld_half_nt halves, in place: every lane
+// adds its half of K = 0x8080...80; the carry out of an element's low half
+// (lane l < 32) enters its high half (lane l + 32) through one v_permlane32_swap
+// for all N; then the xor. Same bytes as to_digits on the whole element.
+template <int N>
+__device__ __forceinline__ void to_digits_halves(u32x4 (&h)[N]) {
+  static_assert(N <= 32, "one carry bit per value in a 32-bit word");
+  uint32_t cm = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[i][j] = addc32(h[i][j], 0x80808080u, c, &c);
+    cm |= c << i;
+  }
+  // the low half's carries, in the high half's lane (the swap runs with every lane
+  // active: inside the select's branch the low lanes would be masked off)
+  const uint32_t pc = xchg32(cm);
+  const uint32_t cin = (threadIdx.x & 32) ? pc : 0u;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t c = (cin >> i) & 1u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) h[i][j] = addc32(h[i][j], 0u, c, &c) ^ 0x80808080u;
+  }
+}
+__device__ __forceinline__ i32x4 as_i32x4(const u32x4& v) {
+  i32x4 r;
+  r[0] = (int)v[0];
+  r[1] = (int)v[1];
+  r[2] = (int)v[2];
+  r[3] = (int)v[3];
+  return r;
+}
+
 // The result words after a fold MFMA pair: lane (e, h) holds words 2g + h of
 // both columns (acc0: element e, acc1: element 32 + e); one swap per 32-bit
 // half gives every lane words 2g and 2g + 1 of its own element.
@@ -728,7 +777,10 @@ __device__ __forceinline__ uint64_t t33_group_perm(uint64_t j, uint64_t n3) {  /
 // chunk g, so the pass's LAST reads are whole t33 chunks, which the next step
 // (order 1: chunks in reverse) reads FIRST, while the 256 MB Infinity Cache may
 // still hold them. Any order gives the same sums (exact integer tiles).
-template <class F>
+// LC (ZK_LC_LOADS): the corners load as whole lines with the non-temporal
+// policy (ld_half_nt: lane l holds half l >> 5 of octant l & 31's corner, for
+// both tables) and each lane writes its half digit row.
+template <class F, bool LC = false>
 __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t O,
                                                       uint32_t order, RoundSink sink) {
@@ -754,25 +806,35 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   };
   uint64_t ch = blockIdx.x >> 1;
   Fe cn[2];
-  if (ch < nch) {
-    const uint64_t pc = phys(ch);
-    ZK_DCHECK(pc * 32 + ql + (2 * w + 1) * O < 8 * O);
-    cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
-    cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
-  }
-  uint32_t buf = 0;
-  for (; ch < nch; ch += nb, buf ^= 1) {
+  u32x4 hn[4];  // (LC) corner 2w + (i >> 1) of table i & 1 (X, Y): this lane's half
+  const Fe* __restrict__ TX = pp ? M : A;
+  const Fe* __restrict__ TY = pp ? P : S;
+  auto load = [&](uint64_t pc) {
+    ZK_DCHECK(pc * 32 + 31 + (2 * w + 1) * O < 8 * O);
+    if constexpr (LC) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      to_digits(cn[i]);
-      st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
-    }
-    if (ch + nb < nch) {  // the next chunk's corners, in flight during this chunk's products
-      const uint64_t pc = phys(ch + nb);
-      ZK_DCHECK(pc * 32 + ql + (2 * w + 1) * O < 8 * O);
+      for (int i = 0; i < 4; ++i) hn[i] = ld_half_nt((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
+    } else {
       cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
       cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
     }
+  };
+  if (ch < nch) load(phys(ch));
+  uint32_t buf = 0;
+  for (; ch < nch; ch += nb, buf ^= 1) {
+    if constexpr (LC) {
+      to_digits_halves<4>(hn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<u32x4*>(&sc.img[buf][2 * w + (i >> 1)][i & 1][ql][16 * half]) = hn[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        to_digits(cn[i]);
+        st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
+      }
+    }
+    if (ch + nb < nch) load(phys(ch + nb));  // the next chunk's corners, in flight during this chunk's products
     __syncthreads();  // the image of this chunk is complete (double buffering: one barrier per chunk)
     d0t_mfmas(sc.img[buf], acc);
   }
@@ -938,7 +1000,11 @@ struct T33ScratchP {
   Fe eqw[8];
 };
 
-template <class F, int OCT, bool PIPE = false>
+// LC (ZK_LC_LOADS, the pipelined 64-octant loop): a fold's eight inputs load
+// as whole lines with the non-temporal policy straight into the fold MFMAs' B
+// operands (ld_half_nt: elements ch 64 + u O + [0, 32) and + [32, 64) of each
+// input; to_digits_halves) instead of one element per lane (fold_operands).
+template <class F, int OCT, bool PIPE = false, bool LC = false>
 __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P,
                                                       Fe* __restrict__ A2, Fe* __restrict__ S2, Fe* __restrict__ M2,
@@ -990,10 +1056,26 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       x[k] = ld_fe(X, e + k * h8);
     }
   };
+  // (LC) the halves of fold u's inputs: [k] elements ch 64 + u O + k 8 O + [0, 32), [8 + k] + [32, 64)
+  auto unit_lc = [&](uint64_t ch, int u, u32x4 (&h)[16]) {
+    ch = pch(ch < nch ? ch : 0);
+    const uint64_t e0 = ch * 64 + (uint64_t)u * O;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ZK_DCHECK(e0 + 63 + k * h8 < 8 * h8);
+      h[k] = ld_half_nt(X, e0 + k * h8);
+      h[8 + k] = ld_half_nt(X, e0 + 32 + k * h8);
+    }
+  };
+  static_assert(!LC || (PIPE && OCT == 64), "lane-contiguous loads: the pipelined 64-octant loop");
   Fe nx[8], nx2[8];
+  u32x4 ux[16], ux2[16];
   const bool early = (uint64_t)blockIdx.x < nch && (blockIdx.x != 0 || w != 0);
   auto first_loads = [&]() {
-    if constexpr (OCT == 64) {
+    if constexpr (LC) {
+      unit_lc(blockIdx.x, 0, ux);
+      unit_lc(blockIdx.x, 1, ux2);
+    } else if constexpr (OCT == 64) {
       unit_at(blockIdx.x, 0, nx);
       unit_at(blockIdx.x, 1, nx2);
     } else {
@@ -1049,7 +1131,25 @@ __global__ __launch_bounds__(kBlock, 1) void k_gkr_t33(const Fe* __restrict__ A,
       i32x16 a0, a1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0;
-      {
+      if constexpr (LC) {
+        u32x4 x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          x[k] = ux[k];
+          ux[k] = ux2[k];
+        }
+        const int u2 = f + 2;  // the fold two ahead
+        if (u2 < 8)
+          unit_lc(ch, u2, ux2);
+        else
+          unit_lc(ch + gridDim.x, u2 - 8, ux2);
+        to_digits_halves<16>(x);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], as_i32x4(x[c]), a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(wf[c], as_i32x4(x[8 + c]), a1, 0, 0, 0);
+        }
+      } else {
         Fe x[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
