@@ -317,6 +317,11 @@ __device__ __forceinline__ u32x4 ld_half_nt(const Fe* __restrict__ X, uint64_t e
   const uint32_t l = threadIdx.x & 63;
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X) + 2 * (e0 + (l & 31)) + (l >> 5));
 }
+// the same with the default policy (lines stay in the Infinity Cache for the next pass)
+__device__ __forceinline__ u32x4 ld_half(const Fe* __restrict__ X, uint64_t e0) {
+  const uint32_t l = threadIdx.x & 63;
+  return *(reinterpret_cast<const u32x4*>(X) + 2 * (e0 + (l & 31)) + (l >> 5));
+}
 // digits (to_digits) of N values held as ld_half_nt halves, in place: every lane
 // adds its half of K = 0x8080...80; the carry out of an element's low half
 // (lane l < 32) enters its high half (lane l + 32) through one v_permlane32_swap
@@ -779,11 +784,13 @@ __device__ __forceinline__ uint64_t t33_group_perm(uint64_t j, uint64_t n3) {  /
 // still hold them. Any order gives the same sums (exact integer tiles).
 // LC (ZK_LC_LOADS): the corners load as whole lines with the non-temporal
 // policy (ld_half_nt: lane l holds half l >> 5 of octant l & 31's corner, for
-// both tables) and each lane writes its half digit row.
+// both tables) and each lane writes its half digit row; logical chunks from
+// nt_end on load with the default policy instead, so that the Infinity Cache
+// holds them for the next pass (ZK_D0T_MALL_TAIL, with ZK_MALL_ORDER's order).
 template <class F, bool LC = false>
 __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t O,
-                                                      uint32_t order, RoundSink sink) {
+                                                      uint32_t order, uint64_t nt_end, RoundSink sink) {
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   __shared__ D0TScratch sc;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, half = l >> 5, ql = l & 31;
@@ -809,17 +816,23 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   u32x4 hn[4];  // (LC) corner 2w + (i >> 1) of table i & 1 (X, Y): this lane's half
   const Fe* __restrict__ TX = pp ? M : A;
   const Fe* __restrict__ TY = pp ? P : S;
-  auto load = [&](uint64_t pc) {
+  auto load = [&](uint64_t q) {  // logical chunk q
+    const uint64_t pc = phys(q);
     ZK_DCHECK(pc * 32 + 31 + (2 * w + 1) * O < 8 * O);
     if constexpr (LC) {
+      if (q < nt_end) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) hn[i] = ld_half_nt((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
+        for (int i = 0; i < 4; ++i) hn[i] = ld_half_nt((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hn[i] = ld_half((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
+      }
     } else {
       cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
       cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
     }
   };
-  if (ch < nch) load(phys(ch));
+  if (ch < nch) load(ch);
   uint32_t buf = 0;
   for (; ch < nch; ch += nb, buf ^= 1) {
     if constexpr (LC) {
@@ -834,7 +847,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
         st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
       }
     }
-    if (ch + nb < nch) load(phys(ch + nb));  // the next chunk's corners, in flight during this chunk's products
+    if (ch + nb < nch) load(ch + nb);  // the next chunk's corners, in flight during this chunk's products
     __syncthreads();  // the image of this chunk is complete (double buffering: one barrier per chunk)
     d0t_mfmas(sc.img[buf], acc);
   }
