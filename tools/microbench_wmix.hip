@@ -430,11 +430,13 @@ int main(int argc, char** argv) {
         const float rl = run_pf<8, 8, false, true>(t, O8, grid, reps), rln = run_pf<8, 8, false, true, false, false, false, true>(t, O8, grid, reps);
         const float we = run_pf<8, 8, true>(t, O8, grid, reps), wen = run_pf<8, 8, true, false, false, false, false, true>(t, O8, grid, reps);
         const float wl = run_pf<8, 8, true, true>(t, O8, grid, reps), wln = run_pf<8, 8, true, true, false, false, false, true>(t, O8, grid, reps);
+        const float wlls = run_pf<8, 8, true, true, true, false, false, true>(t, O8, grid, reps);  // + whole-line stores
         auto r_ = [&](float us) { return rd / us / 1e6; };
         auto w_ = [&](float us) { return (rd + wr8) / us / 1e6; };
         printf("regs grid %4d: R8 elem %6.1f (%.2f) nt %6.1f (%.2f) | R8 lane-contig %6.1f (%.2f) nt %6.1f (%.2f) | W8 elem %6.1f (%.2f) "
-               "nt %6.1f (%.2f) | W8 lane-contig %6.1f (%.2f) nt %6.1f (%.2f)\n",
-               grid, re, r_(re), ren, r_(ren), rl, r_(rl), rln, r_(rln), we, w_(we), wen, w_(wen), wl, w_(wl), wln, w_(wln));
+               "nt %6.1f (%.2f) | W8 lane-contig %6.1f (%.2f) nt %6.1f (%.2f) | + lane-contig stores %6.1f (%.2f)\n",
+               grid, re, r_(re), ren, r_(ren), rl, r_(rl), rln, r_(rln), we, w_(we), wen, w_(wen), wl, w_(wl), wln, w_(wln),
+               wlls, w_(wlls));
         fflush(stdout);
       }
     return 0;
