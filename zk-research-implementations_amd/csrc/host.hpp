@@ -227,7 +227,6 @@ struct zk_ctx {
   // ZK_LC_LOADS: lane-contiguous non-temporal input loads (mfma.hpp ld_half_nt) —
   // bit 0 k_gkr_d0t, bit 1 the first k_gkr_t33 (over the input tables), bit 2 the later 64-octant ones
   uint32_t lc_loads = 7;
-  uint32_t d0t_mall_tail = 0;  // ZK_D0T_MALL_TAIL: k_gkr_d0t's last tail/64 of its chunks with the default load policy
   uint32_t mall_order = 0;  // ZK_MALL_ORDER: k_gkr_d0t reads the first k_gkr_t33's chunks grouped, that t33 walks them in reverse; 2: the groups permuted for the second t33 too (mfma.hpp)
   uint32_t t33_oct64_min = 1;  // k_gkr_t33 takes 64-octant chunks from this many chunks per CU (ZK_T33_OCT64_MIN; fewer: 32-octant chunks, twice the chunks; round 6: 4 -> 1, the second pass 2 us faster, profiles/r6_knob_ab.txt)
   uint32_t host_rounds = 4;  // the last <= this many rounds (even) on the host, from tables the persistent tail hands over (ZK_HOST_ROUNDS; 0 off)
@@ -1101,13 +1100,10 @@ void gkr_phase(zk_ctx* c, const Fe* cur[4], uint32_t nv, uint32_t k0, bool acros
                                                 : grid_for(c, 2 * nch * zk::kBlock, zk::k_gkr_d0t<F>)) & ~1u;
       const uint32_t grid = step_grid(c, res, std::max<uint64_t>(2, 2 * ((nch + zk::kD0TChunksMax - 1) / zk::kD0TChunksMax))) & ~1u;
       const uint32_t order = d0t_order;
-      const uint64_t nt_end = nch - nch * std::min<uint32_t>(c->d0t_mall_tail, 64u) / 64;
       if (c->lc_loads & 1u)
-        launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F, true>, grid, cur[0], cur[1], cur[2], cur[3], O, order,
-               nt_end, sk);
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F, true>, grid, cur[0], cur[1], cur[2], cur[3], O, order, sk);
       else
-        launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, order,
-               nt_end, sk);
+        launch(c, ZK_K_GKR_D0, 128.0 * size, 8.0 * size, zk::k_gkr_d0t<F>, grid, cur[0], cur[1], cur[2], cur[3], O, order, sk);
       enqueue_reduce(c, sk, across_ranks, zk::kD0TLimbs);
       return;
     }

@@ -317,11 +317,7 @@ __device__ __forceinline__ u32x4 ld_half_nt(const Fe* __restrict__ X, uint64_t e
   const uint32_t l = threadIdx.x & 63;
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(X) + 2 * (e0 + (l & 31)) + (l >> 5));
 }
-// the same with the default policy (lines stay in the Infinity Cache for the next pass)
-__device__ __forceinline__ u32x4 ld_half(const Fe* __restrict__ X, uint64_t e0) {
-  const uint32_t l = threadIdx.x & 63;
-  return *(reinterpret_cast<const u32x4*>(X) + 2 * (e0 + (l & 31)) + (l >> 5));
-}
+
 // digits (to_digits) of N values held as ld_half_nt halves, in place: every lane
 // adds its half of K = 0x8080...80; the carry out of an element's low half
 // (lane l < 32) enters its high half (lane l + 32) through one v_permlane32_swap
@@ -784,13 +780,19 @@ __device__ __forceinline__ uint64_t t33_group_perm(uint64_t j, uint64_t n3) {  /
 // still hold them. Any order gives the same sums (exact integer tiles).
 // LC (ZK_LC_LOADS): the corners load as whole lines with the non-temporal
 // policy (ld_half_nt: lane l holds half l >> 5 of octant l & 31's corner, for
-// both tables) and each lane writes its half digit row; logical chunks from
-// nt_end on load with the default policy instead, so that the Infinity Cache
-// holds them for the next pass (ZK_D0T_MALL_TAIL, with ZK_MALL_ORDER's order).
+// both tables), ZK_D0T_AHEAD chunks ahead (2 measured 1.001-1.021 against
+// 0.993-1.009 ms per proof for 1, profiles/r6_d0t_ahead_ab.txt), and each lane
+// writes its half digit row.
+// (Measured and removed: the last 1/8 of the chunks read with the default
+// policy, so the Infinity Cache would keep them for the first k_gkr_t33 —
+// profiles/r6_lc_mall_tail_ab.txt.)
+#ifndef ZK_D0T_AHEAD
+#define ZK_D0T_AHEAD 1
+#endif
 template <class F, bool LC = false>
 __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A, const Fe* __restrict__ S,
                                                       const Fe* __restrict__ M, const Fe* __restrict__ P, uint64_t O,
-                                                      uint32_t order, uint64_t nt_end, RoundSink sink) {
+                                                      uint32_t order, RoundSink sink) {
   if (blockIdx.x == 0) ZK_SINK_STAMP(sink, 0);
   __shared__ D0TScratch sc;
   const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63, half = l >> 5, ql = l & 31;
@@ -813,41 +815,50 @@ __global__ __launch_bounds__(kBlock, 2) void k_gkr_d0t(const Fe* __restrict__ A,
   };
   uint64_t ch = blockIdx.x >> 1;
   Fe cn[2];
-  u32x4 hn[4];  // (LC) corner 2w + (i >> 1) of table i & 1 (X, Y): this lane's half
+  // (LC) hn[a][i]: corner 2w + (i >> 1) of table i & 1 (X, Y), this lane's half, a chunks ahead
+  u32x4 hn[ZK_D0T_AHEAD][4];
   const Fe* __restrict__ TX = pp ? M : A;
   const Fe* __restrict__ TY = pp ? P : S;
+  auto load_lc = [&](uint64_t q, u32x4 (&h)[4]) {  // logical chunk q (past the end: chunk 0, every block the same lines)
+    const uint64_t pc = phys(q < nch ? q : 0);
+    ZK_DCHECK(pc * 32 + 31 + (2 * w + 1) * O < 8 * O);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = ld_half_nt((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
+  };
   auto load = [&](uint64_t q) {  // logical chunk q
     const uint64_t pc = phys(q);
     ZK_DCHECK(pc * 32 + 31 + (2 * w + 1) * O < 8 * O);
-    if constexpr (LC) {
-      if (q < nt_end) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) hn[i] = ld_half_nt((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) hn[i] = ld_half((i & 1) ? TY : TX, pc * 32 + (2 * w + (i >> 1)) * O);
-      }
-    } else {
-      cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
-      cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
-    }
+    cn[0] = ld_fe(T, pc * 32 + ql + (2 * w) * O);
+    cn[1] = ld_fe(T, pc * 32 + ql + (2 * w + 1) * O);
   };
-  if (ch < nch) load(ch);
+  if (ch < nch) {
+    if constexpr (LC) {
+#pragma unroll
+      for (int a = 0; a < ZK_D0T_AHEAD; ++a) load_lc(ch + a * nb, hn[a]);
+    } else {
+      load(ch);
+    }
+  }
   uint32_t buf = 0;
   for (; ch < nch; ch += nb, buf ^= 1) {
     if constexpr (LC) {
-      to_digits_halves<4>(hn);
+      to_digits_halves<4>(hn[0]);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<u32x4*>(&sc.img[buf][2 * w + (i >> 1)][i & 1][ql][16 * half]) = hn[i];
+        *reinterpret_cast<u32x4*>(&sc.img[buf][2 * w + (i >> 1)][i & 1][ql][16 * half]) = hn[0][i];
+#pragma unroll
+      for (int a = 0; a + 1 < ZK_D0T_AHEAD; ++a)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hn[a][i] = hn[a + 1][i];
+      load_lc(ch + ZK_D0T_AHEAD * nb, hn[ZK_D0T_AHEAD - 1]);  // in flight during this chunk's products
     } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         to_digits(cn[i]);
         st_row(&sc.img[buf][2 * w + i][half][ql][0], cn[i]);
       }
+      if (ch + nb < nch) load(ch + nb);  // the next chunk's corners, in flight during this chunk's products
     }
-    if (ch + nb < nch) load(ch + nb);  // the next chunk's corners, in flight during this chunk's products
     __syncthreads();  // the image of this chunk is complete (double buffering: one barrier per chunk)
     d0t_mfmas(sc.img[buf], acc);
   }

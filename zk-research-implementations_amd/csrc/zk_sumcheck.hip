@@ -64,7 +64,6 @@ int zk_ctx_create(int device, zk_ctx** out) {
     if (const char* e = getenv("ZK_MSM_WIN_TASK")) c->msm_win_task = std::max<uint32_t>(2u, (uint32_t)strtoul(e, nullptr, 0));
     if (const char* e = getenv("ZK_T33_OCT64_MIN")) c->t33_oct64_min = (uint32_t)strtoul(e, nullptr, 0);
     if (const char* e = getenv("ZK_LC_LOADS")) c->lc_loads = (uint32_t)strtoul(e, nullptr, 0) & 7u;
-    if (const char* e = getenv("ZK_D0T_MALL_TAIL")) c->d0t_mall_tail = std::min<uint32_t>((uint32_t)strtoul(e, nullptr, 0), 64u);
     if (const char* e = getenv("ZK_MALL_ORDER")) c->mall_order = std::min<uint32_t>((uint32_t)strtoul(e, nullptr, 0), 2u);
     if (const char* e = getenv("ZK_HOST_ROUNDS"))  // (<= 8: the tail hands over 4 x 2^(H+2) elements)
       c->host_rounds = std::min<uint32_t>((uint32_t)strtoul(e, nullptr, 0), 8u);
