@@ -166,6 +166,37 @@ def test_mall_order_matches(monkeypatch, case, order):
         assert blob_digest(0, polys, chal) == g["blob_keccak256"]
 
 
+@pytest.mark.parametrize("lc", ["0", "1", "2", "4"])
+@pytest.mark.parametrize("case", [("oracle", 0, 20, "0"), ("oracle", 0, 21, "5"), ("oracle", 2, 20, "3"),
+                                  ("fixture", 0, 24, "0")])
+def test_lc_loads_match(monkeypatch, case, lc):
+    """ZK_LC_LOADS (default 7: all three bits) selects, per kernel, the
+    whole-line non-temporal input loads that land straight in the fold
+    MFMA operands (bit 0 k_gkr_d0t, bit 1 the first k_gkr_t33, bit 2 the
+    later 64-octant ones) or the element-per-lane loads; every other test runs
+    the default, this one each bit alone and none: the oracle's proof at 20
+    and 21 variables (BN254 Fr and BLS12-381 Fr; grid-capped so blocks take
+    several chunks and the clamped prefetch runs past their last one) and the
+    24-variable fixture."""
+    kind, field, n, cap = case
+    monkeypatch.setenv("ZK_LC_LOADS", lc)
+    if cap != "0":
+        monkeypatch.setenv("ZK_GRID_CAP", cap)
+    c = zk_amd.Context(0)
+    try:
+        seed = {24: 3}.get(n, 23)
+        got = device_proof(c, field, n, seed)
+    finally:
+        c.close()
+    if kind == "oracle":
+        assert got == oracle_proof(field, n, seed)
+    else:
+        g = LARGE[f"bn254_fr_{n}_s{seed}"]
+        polys, chal = got
+        assert chal == [h2i(x) for x in g["challenges"]]
+        assert blob_digest(0, polys, chal) == g["blob_keccak256"]
+
+
 def test_grid_capped_headline_matches_fixture(monkeypatch):
     g = LARGE["bn254_fr_24_s3"]
     monkeypatch.setenv("ZK_GRID_CAP", "37")  # every step several chunks per block, odd grids
